@@ -1,0 +1,277 @@
+"""oracle — TEST INFRASTRUCTURE ONLY.
+
+ctypes binding of the plain-C CPU checker in this directory:
+
+* ``mpc_condense.c`` restates the condensed-QP construction of LukeSchmitt96/solveMPC
+  (src/ModelPredictiveControlAPI.cpp:111-375), pinned against the known-answer values of
+  SURVEY.md Appendix B;
+* ``osqp_dense.c`` restates OSQP v0.6's ADMM (the un-vendored solver behind
+  ModelPredictiveControlAPI.cpp:51-64,96-105) in dense fp64.  PARITY UNPINNED at that
+  boundary (no OSQP build, no reference fixtures); certified by KKT optimality checks.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may
+import this package, and only as the checker / the timed CPU baseline.  The product
+(``solvempc_amd``) never imports it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+_LIB = None
+
+SOLVED, SOLVED_INACCURATE, MAX_ITER_REACHED = 1, 2, -2
+PRIMAL_INFEASIBLE, DUAL_INFEASIBLE, NON_CVX, UNSOLVED = -3, -4, -7, -10
+
+
+class Settings(C.Structure):
+    _fields_ = [
+        ("rho", C.c_double), ("sigma", C.c_double), ("alpha", C.c_double),
+        ("eps_abs", C.c_double), ("eps_rel", C.c_double),
+        ("eps_prim_inf", C.c_double), ("eps_dual_inf", C.c_double),
+        ("adaptive_rho_tolerance", C.c_double), ("adaptive_rho_fraction", C.c_double),
+        ("max_iter", C.c_int), ("check_termination", C.c_int), ("scaling", C.c_int),
+        ("adaptive_rho", C.c_int), ("adaptive_rho_interval", C.c_int),
+        ("warm_start", C.c_int), ("scaled_termination", C.c_int),
+    ]
+
+
+class Info(C.Structure):
+    _fields_ = [
+        ("iter", C.c_int), ("status", C.c_int), ("rho_updates", C.c_int),
+        ("pri_res", C.c_double), ("dua_res", C.c_double),
+        ("rho_estimate", C.c_double), ("rho", C.c_double),
+    ]
+
+
+class _Plant(C.Structure):
+    _fields_ = [
+        ("nx", C.c_int), ("N", C.c_int), ("s_rows", C.c_int),
+        ("Ad", C.POINTER(C.c_double)), ("Bd", C.POINTER(C.c_double)),
+        ("Cd", C.POINTER(C.c_double)), ("K", C.POINTER(C.c_double)),
+        ("Q", C.c_double), ("R", C.c_double), ("RD", C.c_double),
+    ]
+
+
+class _Ops(C.Structure):
+    _fields_ = [(k, C.POINTER(C.c_double)) for k in
+                ("P", "A", "Fx", "Fu", "Fr", "Sbar", "Ku", "W0", "Su", "Sx")]
+
+
+def lib() -> C.CDLL:
+    """Load (building on first use if needed) oracle/liboracle.so."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    so = _HERE / "liboracle.so"
+    srcs = [_HERE / f for f in ("mpc_condense.c", "osqp_dense.c", "mpc_condense.h", "osqp_dense.h")]
+    if not so.exists() or any(s.stat().st_mtime > so.stat().st_mtime for s in srcs if s.exists()):
+        subprocess.run(["make", "-C", str(_HERE), "-s"], check=True)
+    L = C.CDLL(str(so))
+    dp = C.POINTER(C.c_double)
+    ip = C.POINTER(C.c_int)
+    L.ora_default_settings.argtypes = [C.POINTER(Settings)]
+    L.ora_setup.restype = C.c_void_p
+    L.ora_setup.argtypes = [C.c_int, C.c_int, dp, dp, dp, dp, dp, C.POINTER(Settings)]
+    L.ora_cleanup.argtypes = [C.c_void_p]
+    L.ora_update_lin_cost.argtypes = [C.c_void_p, dp]
+    L.ora_update_upper_bound.argtypes = [C.c_void_p, dp]
+    L.ora_update_lower_bound.argtypes = [C.c_void_p, dp]
+    L.ora_update_bounds.argtypes = [C.c_void_p, dp, dp]
+    L.ora_warm_start.argtypes = [C.c_void_p, dp, dp]
+    L.ora_cold_start.argtypes = [C.c_void_p]
+    L.ora_solve.argtypes = [C.c_void_p]
+    L.ora_solution_x.restype = dp
+    L.ora_solution_x.argtypes = [C.c_void_p]
+    L.ora_solution_y.restype = dp
+    L.ora_solution_y.argtypes = [C.c_void_p]
+    L.ora_get_info.argtypes = [C.c_void_p, C.POINTER(Info)]
+    L.ora_get_scaling.argtypes = [C.c_void_p, dp, dp, dp]
+    L.ora_get_iterates.argtypes = [C.c_void_p, dp, dp, dp]
+    L.ora_batch_solve.restype = C.c_int
+    L.ora_batch_solve.argtypes = [C.c_int, C.c_int, dp, dp, dp, dp, dp, C.POINTER(Settings),
+                                  C.c_int, dp, dp, dp, ip, ip, dp, C.c_int]
+    L.ora_condense.argtypes = [C.POINTER(_Plant), C.POINTER(_Ops)]
+    L.ora_condense.restype = C.c_int
+    L.ora_matpow.argtypes = [C.c_int, dp, C.c_int, dp]
+    _LIB = L
+    return L
+
+
+def _dp(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _ip(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_int))
+
+
+def _c64(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+
+
+def default_settings(**over) -> Settings:
+    s = Settings()
+    lib().ora_default_settings(C.byref(s))
+    for k, v in over.items():
+        setattr(s, k, v)
+    return s
+
+
+# ----------------------------------------------------------------------------- condensing
+def load_plant(path: str | os.PathLike) -> dict:
+    """Read the plant/weights from an MPC_API.json-shaped file (numbers only)."""
+    cfg = json.loads(Path(path).read_text())
+    return {
+        "Ad": np.asarray(cfg["Ad"], dtype=np.float64).reshape(4, 4),
+        "Bd": np.asarray(cfg["Bd"], dtype=np.float64).reshape(4),
+        "Cd": np.asarray(cfg["Cd"], dtype=np.float64).reshape(4),
+        "K": np.asarray(cfg["K"], dtype=np.float64).reshape(4),
+        "Q": float(np.asarray(cfg["Q"]).reshape(-1)[0]),
+        "R": float(np.asarray(cfg["R"]).reshape(-1)[0]),
+        "RD": float(np.asarray(cfg["RD"]).reshape(-1)[0]),
+        "xref": float(cfg.get("xref", 0.0)),
+    }
+
+
+def condense(plant: dict, N: int, s_rows: int = 10) -> dict:
+    """Condensed operators (ModelPredictiveControlAPI.cpp:180-368) as fp64 numpy arrays."""
+    nx = plant["Ad"].shape[0]
+    keep = {k: _c64(plant[k]) for k in ("Ad", "Bd", "Cd", "K")}
+    pl = _Plant(nx, N, s_rows, _dp(keep["Ad"]), _dp(keep["Bd"]), _dp(keep["Cd"]), _dp(keep["K"]),
+                plant["Q"], plant["R"], plant["RD"])
+    shapes = {"P": (N, N), "A": (2 * N, N), "Fx": (N, nx), "Fu": (N,), "Fr": (N, N),
+              "Sbar": (2 * N, nx), "Ku": (2 * N,), "W0": (2 * N,), "Su": (N, N), "Sx": (N, nx)}
+    out = {k: np.zeros(s, dtype=np.float64) for k, s in shapes.items()}
+    ops = _Ops(*[_dp(out[k]) for k in ("P", "A", "Fx", "Fu", "Fr", "Sbar", "Ku", "W0", "Su", "Sx")])
+    if lib().ora_condense(C.byref(pl), C.byref(ops)) != 0:
+        raise ValueError("condense failed")
+    return out
+
+
+def gradient(ops: dict, X, U, xref: float = 0.0) -> np.ndarray:
+    """q = Fx X + Fu U + Fr ref' (setF, ModelPredictiveControlAPI.cpp:372-375).  Batched in X."""
+    X = np.asarray(X, dtype=np.float64)
+    U = np.asarray(U, dtype=np.float64)
+    ref = np.full(ops["Fr"].shape[1], xref)
+    return X @ ops["Fx"].T + U[..., None] * ops["Fu"] + ops["Fr"] @ ref
+
+
+def upper_bound(ops: dict, X, U) -> np.ndarray:
+    """u = W0 + Sbar X + Ku U (ModelPredictiveControlAPI.cpp:43,99).  Batched in X."""
+    X = np.asarray(X, dtype=np.float64)
+    U = np.asarray(U, dtype=np.float64)
+    return ops["W0"] + X @ ops["Sbar"].T + U[..., None] * ops["Ku"]
+
+
+# ----------------------------------------------------------------------------- OSQP restatement
+class Solver:
+    """Single-QP OSQP-0.6 restatement (osqp-eigen call surface as used by the reference)."""
+
+    def __init__(self, P, q, A, l, u, settings: Settings | None = None):
+        self.P, self.q, self.A = _c64(P), _c64(q), _c64(A)
+        self.l, self.u = _c64(l), _c64(u)
+        self.n, self.m = self.P.shape[0], self.A.shape[0]
+        self.settings = settings or default_settings()
+        self._w = lib().ora_setup(self.n, self.m, _dp(self.P), _dp(self.q), _dp(self.A),
+                                  _dp(self.l), _dp(self.u), C.byref(self.settings))
+        if not self._w:
+            raise ValueError("ora_setup rejected the problem data")
+
+    def __del__(self):
+        w = getattr(self, "_w", None)
+        if w:
+            lib().ora_cleanup(w)
+            self._w = None
+
+    def update_gradient(self, q) -> bool:
+        q = _c64(q)
+        return lib().ora_update_lin_cost(self._w, _dp(q)) == 0
+
+    def update_upper_bound(self, u) -> bool:
+        u = _c64(u)
+        return lib().ora_update_upper_bound(self._w, _dp(u)) == 0
+
+    def update_lower_bound(self, l) -> bool:
+        l = _c64(l)
+        return lib().ora_update_lower_bound(self._w, _dp(l)) == 0
+
+    def update_bounds(self, l, u) -> bool:
+        l, u = _c64(l), _c64(u)
+        return lib().ora_update_bounds(self._w, _dp(l), _dp(u)) == 0
+
+    def warm_start(self, x, y):
+        x, y = _c64(x), _c64(y)
+        lib().ora_warm_start(self._w, _dp(x), _dp(y))
+
+    def cold_start(self):
+        lib().ora_cold_start(self._w)
+
+    def solve(self) -> int:
+        lib().ora_solve(self._w)
+        return self.info().status
+
+    def x(self) -> np.ndarray:
+        return np.ctypeslib.as_array(lib().ora_solution_x(self._w), shape=(self.n,)).copy()
+
+    def y(self) -> np.ndarray:
+        return np.ctypeslib.as_array(lib().ora_solution_y(self._w), shape=(self.m,)).copy()
+
+    def info(self) -> Info:
+        i = Info()
+        lib().ora_get_info(self._w, C.byref(i))
+        return i
+
+    def scaling(self):
+        D, E, c = np.zeros(self.n), np.zeros(self.m), C.c_double()
+        lib().ora_get_scaling(self._w, _dp(D), _dp(E), C.byref(c))
+        return D, E, c.value
+
+    def iterates(self):
+        x, z, y = np.zeros(self.n), np.zeros(self.m), np.zeros(self.m)
+        lib().ora_get_iterates(self._w, _dp(x), _dp(z), _dp(y))
+        return x, z, y
+
+
+def batch_solve(P, A, q0, l, u0, q, u, settings: Settings | None = None, nthreads: int = 0):
+    """Shared-template batch: setup(P,q0,A,l,u0) then per QP update q[b], u[b] and solve."""
+    P, A, q0, l, u0 = map(_c64, (P, A, q0, l, u0))
+    q, u = _c64(q), _c64(u)
+    n, m, B = P.shape[0], A.shape[0], q.shape[0]
+    s = settings or default_settings()
+    x = np.zeros((B, n))
+    st = np.zeros(B, dtype=np.int32)
+    it = np.zeros(B, dtype=np.int32)
+    rho = np.zeros(B)
+    rc = lib().ora_batch_solve(n, m, _dp(P), _dp(A), _dp(q0), _dp(l), _dp(u0), C.byref(s), B,
+                               _dp(q), _dp(u), _dp(x), _ip(st), _ip(it), _dp(rho), nthreads)
+    if rc < 0:
+        raise ValueError("ora_batch_solve: setup rejected the data")
+    return x, st, it, rho
+
+
+def kkt_residuals(P, q, A, l, u, x, y) -> dict:
+    """Unscaled KKT residuals of min 1/2 x'Px + q'x s.t. l <= Ax <= u (independent of OSQP)."""
+    P, A = np.asarray(P), np.asarray(A)
+    Pu = np.triu(P)
+    Pf = Pu + np.triu(P, 1).T
+    Ax = A @ x
+    stat = Pf @ x + q + A.T @ y
+    prim = np.maximum(Ax - u, 0) + np.maximum(l - Ax, 0)
+    yp, ym = np.maximum(y, 0), np.minimum(y, 0)
+    dual_sign = np.where(u > 1e20, np.abs(yp), 0) + np.where(l < -1e20, np.abs(ym), 0)
+    finite_u = np.where(u < 1e20, u, 0.0)
+    finite_l = np.where(l > -1e20, l, 0.0)
+    compl = np.abs(yp * (finite_u - Ax) * (u < 1e20)) + np.abs(ym * (finite_l - Ax) * (l > -1e20))
+    return {
+        "stationarity": float(np.abs(stat).max(initial=0.0)),
+        "primal": float(prim.max(initial=0.0)),
+        "dual_sign": float(dual_sign.max(initial=0.0)),
+        "complementarity": float(compl.max(initial=0.0)),
+    }
