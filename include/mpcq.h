@@ -1,0 +1,167 @@
+/*
+ * include/mpcq.h — C ABI of the MI355X (gfx950) batched condensed-MPC QP solver.
+ *
+ * This is the drop-in boundary for the one hot path of LukeSchmitt96/solveMPC: the QP solve that
+ * ModelPredictiveControlAPI performs through osqp-eigen (OsqpEigen::Solver, a member at
+ * include/ModelPredictiveControlAPI.h:144).  Every entry point names the reference call it
+ * replaces.  Conventions:
+ *   - plain pointers and sizes; every function returns an int status, 0 == MPCQ_OK;
+ *   - host buffers are caller-owned and only read/written during the call; device buffers are
+ *     owned by the context;
+ *   - matrices are dense, row-major, fp64 (the reference's c_float == double), QP-major across a
+ *     batch: element (b, i, j) of a batch of r x c matrices sits at b*r*c + i*c + j;
+ *   - one context per host thread; calls on one context are not re-entrant;
+ *   - `stream` is a hipStream_t passed as void* (NULL = the default stream).
+ *
+ * A context holds `batch` independent QPs of identical shape (n variables, m constraints).
+ * They either share one plant (n_plants == 1: one P and A, e.g. 65,536 copies of the reference's
+ * controller fed different states) or carry one plant each (n_plants == batch).
+ */
+#ifndef MPCQ_H
+#define MPCQ_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes -------------------------------------------------------------------------- */
+#define MPCQ_OK 0
+#define MPCQ_ERR_ARG (-1)      /* bad argument / unsupported size                              */
+#define MPCQ_ERR_HIP (-2)      /* HIP runtime error or no usable gfx950 device                 */
+#define MPCQ_ERR_SETUP (-3)    /* setup rejected the data (P not PSD / KKT not quasi-definite) */
+#define MPCQ_ERR_ORDER (-4)    /* call order (e.g. solve before setup)                         */
+#define MPCQ_ERR_BOUNDS (-5)   /* some u < l (osqp_update_*_bound failure)                     */
+
+/* ---- per-QP status (OSQP v0.6 values; osqp-eigen's solve() is true only for SOLVED) ------- */
+#define MPCQ_SOLVED 1
+#define MPCQ_SOLVED_INACCURATE 2
+#define MPCQ_PRIMAL_INFEASIBLE_INACCURATE 3
+#define MPCQ_DUAL_INFEASIBLE_INACCURATE 4
+#define MPCQ_MAX_ITER_REACHED (-2)
+#define MPCQ_PRIMAL_INFEASIBLE (-3)
+#define MPCQ_DUAL_INFEASIBLE (-4)
+#define MPCQ_NON_CVX (-7)
+#define MPCQ_UNSOLVED (-10)
+#define MPCQ_INVALID_BOUNDS (-20) /* this QP's u < l: update rejected, not solved              */
+#define MPCQ_TYPE_CHANGED (-21)   /* this QP's bounds changed a row's OSQP constraint type
+                                     (equality/inequality/free) away from its plant's setup;
+                                     re-run mpcq_setup with these bounds                     */
+
+/* ---- precision of the device iterate ------------------------------------------------------- */
+#define MPCQ_F64 0 /* fp64 throughout (the reference's precision)                            */
+#define MPCQ_F32 1 /* fp32 ADMM iterate, fp64 setup                                           */
+
+/* OSQP v0.6 settings (osqp constants.h defaults via mpcq_default_settings).  Replaces
+ * OsqpEigen::Settings as used at ModelPredictiveControlAPI.cpp:51-52 (setVerbosity,
+ * setWarmStart(true)); polish is not supported (the reference leaves it off). */
+typedef struct mpcq_settings {
+    double rho, sigma, alpha;
+    double eps_abs, eps_rel, eps_prim_inf, eps_dual_inf;
+    double adaptive_rho_tolerance, adaptive_rho_fraction;
+    int max_iter, check_termination, scaling, adaptive_rho, adaptive_rho_interval;
+    int warm_start, scaled_termination, verbose;
+} mpcq_settings;
+
+typedef struct mpcq_dims {
+    int n;        /* decision variables  (setNumberOfVariables, :54)   */
+    int m;        /* constraint rows     (setNumberOfConstraints, :55) */
+    int batch;    /* QPs in this context (reference: 1)                */
+    int n_plants; /* 1 (shared P, A) or batch (one plant per QP)       */
+    int dtype;    /* MPCQ_F64 or MPCQ_F32                              */
+    int device;   /* HIP device ordinal                                */
+} mpcq_dims;
+
+typedef struct mpcq_ctx mpcq_ctx;
+
+/* Device-resident views of a context's buffers (fp64, QP-major), for zero-copy callers. */
+typedef struct mpcq_device_view {
+    double *q;     /* batch*n   gradient (input of the next solve)      */
+    double *u;     /* batch*m   upper bounds                            */
+    double *l;     /* batch*m   lower bounds                            */
+    double *x;     /* batch*n   unscaled primal solution (output)       */
+    double *y;     /* batch*m   unscaled dual solution (output)         */
+    int *status;   /* batch     MPCQ_* status (output)                  */
+    int *iter;     /* batch     ADMM iterations (output)                */
+    double *rho;   /* batch     rho after the solve (output)            */
+} mpcq_device_view;
+
+void mpcq_default_settings(mpcq_settings *s);
+
+/* Allocate a context on dims->device.  Fails with MPCQ_ERR_HIP when no gfx950 device exists. */
+int mpcq_create(const mpcq_dims *dims, const mpcq_settings *settings, mpcq_ctx **out);
+int mpcq_destroy(mpcq_ctx *ctx);
+
+/* Setup: replaces setHessianMatrix / setGradient / setLinearConstraintsMatrix / setLowerBound /
+ * setUpperBound + initSolver (ModelPredictiveControlAPI.cpp:57-64 -> osqp_setup).  Arrays are per
+ * plant (n_plants copies): P n*n (upper triangle read, as osqp-eigen does), q0 n, A m*n, l0/u0 m.
+ * Ruiz equilibration, cost scaling and the KKT factorisation run on the device.  q0/l0/u0 also
+ * become the current q/l/u of every QP of the plant. */
+int mpcq_setup(mpcq_ctx *ctx, const double *P, const double *q0, const double *A,
+               const double *l0, const double *u0);
+
+/* Per-QP data updates from host memory (batch*n or batch*m).
+ * Replace OsqpEigen::Solver::updateGradient (:96 -> osqp_update_lin_cost) and
+ * updateUpperBound (:99 -> osqp_update_upper_bound); lower/both-bound forms for completeness.
+ * Bounds are validated per QP when the solve runs (status MPCQ_INVALID_BOUNDS). */
+int mpcq_update_lin_cost(mpcq_ctx *ctx, const double *q);
+int mpcq_update_upper_bound(mpcq_ctx *ctx, const double *u);
+int mpcq_update_lower_bound(mpcq_ctx *ctx, const double *l);
+int mpcq_update_bounds(mpcq_ctx *ctx, const double *l, const double *u);
+
+/* osqp_warm_start / cold_start for every QP (x batch*n, y batch*m, unscaled). */
+int mpcq_warm_start(mpcq_ctx *ctx, const double *x, const double *y);
+int mpcq_cold_start(mpcq_ctx *ctx);
+
+/* Return every QP to the state right after setup (x = z = y = 0, rho = settings.rho), as
+ * re-running initSolver (:64) would; applied by the next solve at no cost. */
+int mpcq_reset(mpcq_ctx *ctx);
+
+/* Solve every QP (replaces OsqpEigen::Solver::solve, :102 -> osqp_solve).  Asynchronous on
+ * `stream`; iterates stay on the device (warm start, :52). */
+int mpcq_solve(mpcq_ctx *ctx, void *stream);
+
+/* Results (synchronise the context's last stream).  Replace getSolution() (:105). */
+int mpcq_get_solution(mpcq_ctx *ctx, double *x);            /* batch*n */
+int mpcq_get_dual(mpcq_ctx *ctx, double *y);                /* batch*m */
+int mpcq_get_info(mpcq_ctx *ctx, int *status, int *iter, double *rho); /* each batch, may be NULL */
+int mpcq_get_scaling(mpcq_ctx *ctx, double *D, double *E, double *c); /* plant 0: n, m, 1 */
+
+int mpcq_device_view_get(mpcq_ctx *ctx, mpcq_device_view *view);
+
+/* ---- condensed-MPC front end: ModelPredictiveControlAPI::controllerStep, batched ------------
+ * Per-plant operators of the condensed problem (n == N, m == 2N; ModelPredictiveControlAPI.cpp
+ * setFVars :303-307, setUpperBound :360-369, setTransformations :185,208): Fx N*nx, Fu N,
+ * Fr N*N, Sbar m*nx, Ku m, W0 m (n_plants copies each). */
+int mpcq_mpc_set_operators(mpcq_ctx *ctx, int nx, const double *Fx, const double *Fu,
+                           const double *Fr, const double *Sbar, const double *Ku,
+                           const double *W0);
+/* One receding-horizon step for every QP, on device-resident X (batch*nx) and U (batch):
+ *   q = Fx X + Fu U + Fr (xref 1)          (setF :372-375, updateRef :378-380)
+ *   u = W0 + Sbar X + Ku U                 (:93-99)
+ *   solve                                  (:102, warm-started)
+ *   U += x[0] where status == SOLVED       (:105)
+ * X_dev/U_dev are device pointers (fp64). */
+int mpcq_mpc_step_device(mpcq_ctx *ctx, const double *X_dev, double *U_dev, double xref,
+                         void *stream);
+
+/* Host-memory convenience form of mpcq_mpc_step_device (copies in/out, synchronises). */
+int mpcq_mpc_step(mpcq_ctx *ctx, const double *X, double *U, double xref);
+
+/* Condensed-QP construction on device `device` for n_plants SISO plants (ModelPredictiveControlAPI
+ * setTransformations / setLL / setLiftedCosts / setH / setFVars / setLinearConstraints /
+ * setUpperBound, src/ModelPredictiveControlAPI.cpp:158-369).  Inputs per plant: Ad nx*nx, Bd nx,
+ * Cd nx, K nx, Q, R, RD (scalars); N = horizon; s_rows = rows of S filled with K (reference: 10,
+ * :185).  Outputs per plant (host memory, caller-allocated): P N*N, A 2N*N, Fx N*nx, Fu N, Fr N*N,
+ * Sbar 2N*nx, Ku 2N, W0 2N.  nx <= 8. */
+int mpcq_condense(int device, int n_plants, int nx, int N, int s_rows, const double *Ad,
+                  const double *Bd, const double *Cd, const double *K, const double *Q,
+                  const double *R, const double *RD, double *P, double *A, double *Fx, double *Fu,
+                  double *Fr, double *Sbar, double *Ku, double *W0);
+
+/* Last HIP error string of this thread (static storage). */
+const char *mpcq_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPCQ_H */

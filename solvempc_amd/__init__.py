@@ -1,0 +1,177 @@
+"""solvempc_amd — MI355X-native batched condensed-MPC QP solver (drop-in for the QP solve path of
+LukeSchmitt96/solveMPC).
+
+Python mirror of the C ABI in ``include/mpcq.h`` (library ``solvempc_amd/libmpcq.so``, built for
+gfx950).  Names follow the reference's solver interface as it is used in
+src/ModelPredictiveControlAPI.cpp (osqp-eigen: ``updateGradient`` / ``updateUpperBound`` /
+``solve`` / ``getSolution``; OSQP settings and status values).  There is no CPU path: importing works
+anywhere the library exists, but creating a solver needs a gfx950 device and fails loudly otherwise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+from . import _capi
+from ._capi import (  # noqa: F401
+    MPCQ_F32, MPCQ_F64, SOLVED, SOLVED_INACCURATE, MAX_ITER_REACHED, PRIMAL_INFEASIBLE,
+    PRIMAL_INFEASIBLE_INACCURATE, DUAL_INFEASIBLE, DUAL_INFEASIBLE_INACCURATE, NON_CVX, UNSOLVED,
+    INVALID_BOUNDS, TYPE_CHANGED, MpcqError, Settings, lib, library_path,
+)
+
+__all__ = ["BatchSolver", "Settings", "default_settings", "lib", "library_path", "MpcqError"]
+
+
+def default_settings(**over) -> Settings:
+    """OSQP v0.6 defaults + warm start (ModelPredictiveControlAPI.cpp:51-52)."""
+    s = Settings()
+    lib().mpcq_default_settings(C.byref(s))
+    for k, v in over.items():
+        if not hasattr(s, k):
+            raise AttributeError(f"unknown setting {k}")
+        setattr(s, k, v)
+    return s
+
+
+def _c64(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+
+
+def _dp(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+class BatchSolver:
+    """A batch of independent QPs  min 1/2 x'Px + q'x  s.t. l <= Ax <= u  on one gfx950 device.
+
+    ``n_plants == 1``: all QPs share P and A (the reference's controller replicated over many
+    states).  ``n_plants == batch``: one (P, A) per QP.
+    """
+
+    def __init__(self, n: int, m: int, batch: int, n_plants: int = 1, dtype: str = "f64",
+                 device: int = 0, settings: Settings | None = None):
+        self.n, self.m, self.batch, self.n_plants = int(n), int(m), int(batch), int(n_plants)
+        self.dtype = dtype
+        self.settings = settings or default_settings()
+        dims = _capi.Dims(self.n, self.m, self.batch, self.n_plants,
+                          MPCQ_F32 if dtype == "f32" else MPCQ_F64, int(device))
+        ctx = C.c_void_p()
+        _capi.check(lib().mpcq_create(C.byref(dims), C.byref(self.settings), C.byref(ctx)), "mpcq_create")
+        self._ctx = ctx
+        self.nx = 0
+
+    def close(self):
+        ctx = getattr(self, "_ctx", None)
+        if ctx:
+            lib().mpcq_destroy(ctx)
+            self._ctx = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- setup: setHessianMatrix / setGradient / setLinearConstraintsMatrix / set*Bound + initSolver
+    def setup(self, P, q0, A, l0, u0) -> None:
+        k = self.n_plants
+        P = _c64(P).reshape(k, self.n, self.n)
+        q0 = _c64(q0).reshape(k, self.n)
+        A = _c64(A).reshape(k, self.m, self.n)
+        l0 = _c64(l0).reshape(k, self.m)
+        u0 = _c64(u0).reshape(k, self.m)
+        _capi.check(lib().mpcq_setup(self._ctx, _dp(P), _dp(q0), _dp(A), _dp(l0), _dp(u0)), "mpcq_setup")
+
+    # -- per-step updates (updateGradient :96, updateUpperBound :99)
+    def update_lin_cost(self, q) -> None:
+        q = _c64(q).reshape(self.batch, self.n)
+        _capi.check(lib().mpcq_update_lin_cost(self._ctx, _dp(q)), "mpcq_update_lin_cost")
+
+    update_gradient = update_lin_cost
+
+    def update_upper_bound(self, u) -> None:
+        u = _c64(u).reshape(self.batch, self.m)
+        _capi.check(lib().mpcq_update_upper_bound(self._ctx, _dp(u)), "mpcq_update_upper_bound")
+
+    def update_lower_bound(self, l) -> None:
+        l = _c64(l).reshape(self.batch, self.m)
+        _capi.check(lib().mpcq_update_lower_bound(self._ctx, _dp(l)), "mpcq_update_lower_bound")
+
+    def update_bounds(self, l, u) -> None:
+        l = _c64(l).reshape(self.batch, self.m)
+        u = _c64(u).reshape(self.batch, self.m)
+        _capi.check(lib().mpcq_update_bounds(self._ctx, _dp(l), _dp(u)), "mpcq_update_bounds")
+
+    def warm_start(self, x, y) -> None:
+        x = _c64(x).reshape(self.batch, self.n)
+        y = _c64(y).reshape(self.batch, self.m)
+        _capi.check(lib().mpcq_warm_start(self._ctx, _dp(x), _dp(y)), "mpcq_warm_start")
+
+    def cold_start(self) -> None:
+        _capi.check(lib().mpcq_cold_start(self._ctx), "mpcq_cold_start")
+
+    def reset_state(self) -> None:
+        """Back to the post-setup state (x = z = y = 0, rho = settings.rho) for the next solve."""
+        _capi.check(lib().mpcq_reset(self._ctx), "mpcq_reset")
+
+    # -- solve (:102) and results (:105)
+    def solve(self, stream: int | None = None) -> None:
+        _capi.check(lib().mpcq_solve(self._ctx, C.c_void_p(stream or 0)), "mpcq_solve")
+
+    def solution(self) -> np.ndarray:
+        x = np.empty((self.batch, self.n))
+        _capi.check(lib().mpcq_get_solution(self._ctx, _dp(x)), "mpcq_get_solution")
+        return x
+
+    def dual(self) -> np.ndarray:
+        y = np.empty((self.batch, self.m))
+        _capi.check(lib().mpcq_get_dual(self._ctx, _dp(y)), "mpcq_get_dual")
+        return y
+
+    def info(self):
+        st = np.empty(self.batch, dtype=np.int32)
+        it = np.empty(self.batch, dtype=np.int32)
+        rho = np.empty(self.batch)
+        _capi.check(lib().mpcq_get_info(self._ctx, st.ctypes.data_as(C.POINTER(C.c_int)),
+                                        it.ctypes.data_as(C.POINTER(C.c_int)), _dp(rho)), "mpcq_get_info")
+        return st, it, rho
+
+    def scaling(self):
+        D, E, c = np.empty(self.n), np.empty(self.m), C.c_double()
+        _capi.check(lib().mpcq_get_scaling(self._ctx, _dp(D), _dp(E), C.byref(c)), "mpcq_get_scaling")
+        return D, E, c.value
+
+    def device_view(self) -> dict:
+        v = _capi.DeviceView()
+        _capi.check(lib().mpcq_device_view_get(self._ctx, C.byref(v)), "mpcq_device_view_get")
+        return {k: int(getattr(v, k) or 0) for k, _ in _capi.DeviceView._fields_}
+
+    # -- condensed-MPC front end (controllerStep, :81-108)
+    def mpc_set_operators(self, Fx, Fu, Fr, Sbar, Ku, W0) -> None:
+        k = self.n_plants
+        Fx = _c64(Fx).reshape(k, self.n, -1)
+        self.nx = Fx.shape[2]
+        args = [Fx, _c64(Fu).reshape(k, self.n), _c64(Fr).reshape(k, self.n, self.n),
+                _c64(Sbar).reshape(k, self.m, self.nx), _c64(Ku).reshape(k, self.m), _c64(W0).reshape(k, self.m)]
+        _capi.check(lib().mpcq_mpc_set_operators(self._ctx, self.nx, *[_dp(a) for a in args]),
+                    "mpcq_mpc_set_operators")
+
+    def mpc_step(self, X, U, xref: float = 0.0) -> np.ndarray:
+        """One receding-horizon step for every QP from host X (batch, nx), U (batch); returns new U."""
+        X = _c64(X).reshape(self.batch, self.nx)
+        U = _c64(U).reshape(self.batch).copy()
+        _capi.check(lib().mpcq_mpc_step(self._ctx, _dp(X), _dp(U), float(xref)), "mpcq_mpc_step")
+        return U
+
+    def mpc_step_device(self, X_ptr: int, U_ptr: int, xref: float = 0.0, stream: int | None = None) -> None:
+        """Same on device-resident fp64 buffers (e.g. torch tensors' data_ptr()); asynchronous."""
+        _capi.check(lib().mpcq_mpc_step_device(self._ctx, C.c_void_p(X_ptr), C.c_void_p(U_ptr),
+                                               float(xref), C.c_void_p(stream or 0)), "mpcq_mpc_step_device")
+
+
+from .mpc import ModelPredictiveControlAPI, from_json  # noqa: E402,F401

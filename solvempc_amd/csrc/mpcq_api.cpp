@@ -1,0 +1,646 @@
+// solvempc_amd/csrc/mpcq_api.cpp — host side of the C ABI declared in include/mpcq.h.
+//
+// Orchestration only: argument checks, device buffers, kernel launches.  All arithmetic on the
+// QPs (setup, ADMM, MPC front end) runs in the HIP kernels of mpcq_setup.hip / mpcq_admm.hip.
+// There is no CPU solve path: without a gfx950 device mpcq_create fails with MPCQ_ERR_HIP.
+#include "../../include/mpcq.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "mpcq_internal.h"
+
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg)
+{
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                  \
+    do {                                                                              \
+        hipError_t e_ = (expr);                                                       \
+        if (e_ != hipSuccess) return fail(MPCQ_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+size_t setup_scratch_len(int n, int m)
+{
+    return 7 * (size_t)n * n + (size_t)m * n + 3 * (size_t)n + 2 * (size_t)m + 64;
+}
+}  // namespace
+
+struct mpcq_ctx {
+    mpcq_dims dims{};
+    mpcq_settings set{};
+    int nc = 0, mc = 0;
+    size_t ops_stride = 0;
+    bool setup_done = false, all_ineq = true, mpc_ready = false, lower_free = false, fresh = false;
+    hipStream_t last = nullptr;
+    int nx = 0;
+    // setup
+    double *d_P = nullptr, *d_q0 = nullptr, *d_A = nullptr, *d_l0 = nullptr, *d_u0 = nullptr;
+    double *d_ops = nullptr, *d_scratch = nullptr;
+    float *d_ops32 = nullptr;
+    int *d_ctype = nullptr, *d_setup_status = nullptr;
+    // per QP
+    double *d_q = nullptr, *d_u = nullptr, *d_l = nullptr, *d_x = nullptr, *d_y = nullptr, *d_rho = nullptr;
+    int *d_status = nullptr, *d_iter = nullptr;
+    void *d_xs = nullptr, *d_zs = nullptr, *d_ys = nullptr, *d_rhos = nullptr, *d_snx = nullptr, *d_sny = nullptr;
+    // MPC front end
+    double *d_Fx = nullptr, *d_Fu = nullptr, *d_Fr = nullptr, *d_Sbar = nullptr, *d_Ku = nullptr, *d_W0 = nullptr;
+    double *d_X = nullptr, *d_U = nullptr;
+    // host copies of plant-0 scaling
+    std::vector<double> hD, hE;
+    double hc = 1.0;
+};
+
+namespace {
+
+template <typename T>
+void fill_ops(mpcq::PlantOps<T> &op, const T *base, const mpcq::OpsLayout &L, const int *ctype)
+{
+    op.lam = base + L.lam;
+    op.W = base + L.W;
+    op.sWtW = base + L.sWtW;
+    op.WtA = base + L.WtA;
+    op.PW = base + L.PW;
+    op.Winv = base + L.Winv;
+    op.Ah = base + L.Ah;
+    op.D = base + L.D;
+    op.E = base + L.E;
+    op.Dinv = base + L.Dinv;
+    op.Einv = base + L.Einv;
+    op.cs = base + L.cs;
+    op.rscale = base + L.rscale;
+    op.ctype = ctype;
+}
+
+mpcq::SolverSettings to_solver(const mpcq_settings &s)
+{
+    mpcq::SolverSettings o{};
+    o.rho = s.rho;
+    o.sigma = s.sigma;
+    o.alpha = s.alpha;
+    o.eps_abs = s.eps_abs;
+    o.eps_rel = s.eps_rel;
+    o.eps_prim_inf = s.eps_prim_inf;
+    o.eps_dual_inf = s.eps_dual_inf;
+    o.adaptive_rho_tolerance = s.adaptive_rho_tolerance;
+    o.max_iter = s.max_iter;
+    o.check_termination = s.check_termination;
+    o.adaptive_rho = s.adaptive_rho;
+    o.adaptive_rho_interval = s.adaptive_rho_interval;
+    o.warm_start = s.warm_start;
+    o.scaled_termination = s.scaled_termination;
+    o.scaling = s.scaling;
+    return o;
+}
+
+template <typename T>
+mpcq::AdmmArgs<T> make_args(mpcq_ctx *c)
+{
+    mpcq::AdmmArgs<T> a{};
+    const mpcq::OpsLayout L = mpcq::OpsLayout::make(c->nc, c->mc);
+    const T *base = std::is_same<T, double>::value ? (const T *)c->d_ops : (const T *)c->d_ops32;
+    fill_ops(a.ops, base, L, c->d_ctype);
+    a.batch = c->dims.batch;
+    a.n = c->dims.n;
+    a.m = c->dims.m;
+    a.shared = c->dims.n_plants == 1;
+    a.ops_stride = c->ops_stride;
+    a.ctype = c->d_ctype;
+    a.st = to_solver(c->set);
+    const int ct = c->set.check_termination;
+    a.adaptive_interval = c->set.adaptive_rho_interval ? c->set.adaptive_rho_interval : (ct ? 4 * ct : 100);
+    a.all_ineq = c->all_ineq;
+    a.lower_free = c->lower_free;
+    a.q = c->d_q;
+    a.u = c->d_u;
+    a.l = c->d_l;
+    a.l_shared = 0;
+    a.xs = (T *)c->d_xs;
+    a.zs = (T *)c->d_zs;
+    a.ys = (T *)c->d_ys;
+    a.rhos = (T *)c->d_rhos;
+    a.warm = c->set.warm_start;
+    a.fresh = c->fresh;
+    a.snap_x = (T *)c->d_snx;
+    a.snap_y = (T *)c->d_sny;
+    a.x = c->d_x;
+    a.y = c->d_y;
+    a.rho_out = c->d_rho;
+    a.status = c->d_status;
+    a.iter = c->d_iter;
+    return a;
+}
+
+int reset_state(mpcq_ctx *c, bool reset_rho)
+{
+    const size_t B = c->dims.batch, es = c->dims.dtype == MPCQ_F32 ? 4 : 8;
+    HIPCHK(hipMemsetAsync(c->d_xs, 0, es * c->nc * B, c->last));
+    HIPCHK(hipMemsetAsync(c->d_zs, 0, es * c->mc * B, c->last));
+    HIPCHK(hipMemsetAsync(c->d_ys, 0, es * c->mc * B, c->last));
+    if (reset_rho) {
+        const double r = std::min(std::max(c->set.rho, mpcq::kRhoMin), mpcq::kRhoMax);
+        if (mpcq_internal_fill(c->d_rhos, c->dims.dtype == MPCQ_F32, r, B, c->last) != 0)
+            return fail(MPCQ_ERR_HIP, "fill kernel failed");
+    }
+    return MPCQ_OK;
+}
+
+// True when every scaled lower bound is below -OSQP_INFTY*MIN_SCALING (the reference's
+// l = -DBL_MAX, :42), which selects the kernel variant without the lower clamp.  Exact for a
+// shared plant (its E is on the host); conservative (|l| >= 1e300) for per-plant contexts.
+bool lower_all_free(const mpcq_ctx *c, const double *l)
+{
+    const size_t B = (l == nullptr) ? 0 : (size_t)c->dims.m;
+    const size_t rows = c->dims.n_plants == 1 ? B : 0;
+    if (c->dims.n_plants == 1) {
+        for (size_t j = 0; j < rows; j++)
+            if (!(l[j] * c->hE[j] < -mpcq::kInfty * mpcq::kMinScaling)) return false;
+        return true;
+    }
+    return false;
+}
+
+bool lower_all_free_batch(const mpcq_ctx *c, const double *l)
+{
+    const size_t total = (size_t)c->dims.batch * c->dims.m;
+    for (size_t i = 0; i < total; i++) {
+        const double e = c->dims.n_plants == 1 ? c->hE[i % c->dims.m] : 1e-250;
+        if (!(l[i] * e < -mpcq::kInfty * mpcq::kMinScaling) && !(l[i] <= -1e300)) return false;
+    }
+    return true;
+}
+
+int check_ctx(mpcq_ctx *c, bool need_setup)
+{
+    if (!c) return fail(MPCQ_ERR_ARG, "null context");
+    if (need_setup && !c->setup_done) return fail(MPCQ_ERR_ORDER, "mpcq_setup has not succeeded");
+    HIPCHK(hipSetDevice(c->dims.device));
+    return MPCQ_OK;
+}
+
+int h2d(void *dst, const void *src, size_t bytes, hipStream_t s)
+{
+    if (!bytes) return MPCQ_OK;
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return MPCQ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void mpcq_default_settings(mpcq_settings *s)
+{
+    if (!s) return;
+    // osqp constants.h (v0.6) + osqp-eigen setWarmStart(true) (ModelPredictiveControlAPI.cpp:52)
+    s->rho = 0.1;
+    s->sigma = 1e-6;
+    s->alpha = 1.6;
+    s->eps_abs = 1e-3;
+    s->eps_rel = 1e-3;
+    s->eps_prim_inf = 1e-4;
+    s->eps_dual_inf = 1e-4;
+    s->adaptive_rho_tolerance = 5.0;
+    s->adaptive_rho_fraction = 0.4;
+    s->max_iter = 4000;
+    s->check_termination = 25;
+    s->scaling = 10;
+    s->adaptive_rho = 1;
+    s->adaptive_rho_interval = 0;
+    s->warm_start = 1;
+    s->scaled_termination = 0;
+    s->verbose = 0;
+}
+
+const char *mpcq_last_error(void) { return g_err.c_str(); }
+
+int mpcq_create(const mpcq_dims *d, const mpcq_settings *s, mpcq_ctx **out)
+{
+    if (!d || !out) return fail(MPCQ_ERR_ARG, "null argument");
+    *out = nullptr;
+    if (d->n <= 0 || d->m < 0 || d->batch <= 0) return fail(MPCQ_ERR_ARG, "n > 0, m >= 0, batch > 0 required");
+    if (d->n_plants != 1 && d->n_plants != d->batch) return fail(MPCQ_ERR_ARG, "n_plants must be 1 or batch");
+    if (d->dtype != MPCQ_F64 && d->dtype != MPCQ_F32) return fail(MPCQ_ERR_ARG, "dtype");
+    mpcq_settings st;
+    mpcq_default_settings(&st);
+    if (s) st = *s;
+    if (st.rho <= 0 || st.sigma <= 0 || st.alpha <= 0 || st.alpha >= 2 || st.max_iter <= 0 ||
+        st.eps_abs < 0 || st.eps_rel < 0 || (st.eps_abs == 0 && st.eps_rel == 0) || st.scaling < 0 ||
+        st.check_termination < 0 || st.adaptive_rho_tolerance < 1 || st.adaptive_rho_interval < 0)
+        return fail(MPCQ_ERR_ARG, "invalid settings (osqp validate_settings)");
+    int nc = 0, mc = 0;
+    if (mpcq_internal_caps(d->n, std::max(d->m, 1), &nc, &mc) != 0)
+        return fail(MPCQ_ERR_ARG, "n/m exceed the compiled kernel capacities (n <= 32, m <= 64)");
+
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= d->device || d->device < 0)
+        return fail(MPCQ_ERR_HIP, "no HIP device with this ordinal");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, d->device) != hipSuccess)
+        return fail(MPCQ_ERR_HIP, "hipGetDeviceProperties failed");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(MPCQ_ERR_HIP, std::string("device is ") + prop.gcnArchName + ", gfx950 required");
+    HIPCHK(hipSetDevice(d->device));
+
+    mpcq_ctx *c = new mpcq_ctx();
+    c->dims = *d;
+    c->set = st;
+    c->nc = nc;
+    c->mc = mc;
+    const mpcq::OpsLayout L = mpcq::OpsLayout::make(nc, mc);
+    c->ops_stride = L.total;
+    const size_t P = d->n_plants, B = d->batch, n = d->n, m = d->m;
+    const size_t es = d->dtype == MPCQ_F32 ? 4 : 8;
+    bool ok = true;
+    auto A = [&](void **p, size_t bytes) {
+        if (!ok) return;
+        if (hipMalloc(p, std::max<size_t>(bytes, 8)) != hipSuccess) ok = false;
+    };
+    A((void **)&c->d_P, 8 * P * n * n);
+    A((void **)&c->d_q0, 8 * P * n);
+    A((void **)&c->d_A, 8 * P * m * n);
+    A((void **)&c->d_l0, 8 * P * m);
+    A((void **)&c->d_u0, 8 * P * m);
+    A((void **)&c->d_ops, 8 * P * L.total);
+    if (d->dtype == MPCQ_F32) A((void **)&c->d_ops32, 4 * P * L.total);
+    A((void **)&c->d_scratch, 8 * P * setup_scratch_len((int)n, (int)m));
+    A((void **)&c->d_ctype, 4 * P * mc);
+    A((void **)&c->d_setup_status, 4 * P);
+    A((void **)&c->d_q, 8 * B * n);
+    A((void **)&c->d_u, 8 * B * m);
+    A((void **)&c->d_l, 8 * B * m);
+    A((void **)&c->d_x, 8 * B * n);
+    A((void **)&c->d_y, 8 * B * m);
+    A((void **)&c->d_rho, 8 * B);
+    A((void **)&c->d_status, 4 * B);
+    A((void **)&c->d_iter, 4 * B);
+    A(&c->d_xs, es * B * nc);
+    A(&c->d_zs, es * B * mc);
+    A(&c->d_ys, es * B * mc);
+    A(&c->d_rhos, es * B);
+    A(&c->d_snx, es * B * nc);
+    A(&c->d_sny, es * B * mc);
+    if (!ok) {
+        mpcq_destroy(c);
+        return fail(MPCQ_ERR_HIP, "hipMalloc failed");
+    }
+    c->hD.assign(n, 1.0);
+    c->hE.assign(m, 1.0);
+    *out = c;
+    return MPCQ_OK;
+}
+
+int mpcq_destroy(mpcq_ctx *c)
+{
+    if (!c) return MPCQ_OK;
+    (void)hipSetDevice(c->dims.device);
+    void *ptrs[] = {c->d_P, c->d_q0, c->d_A, c->d_l0, c->d_u0, c->d_ops, c->d_ops32, c->d_scratch, c->d_ctype,
+                    c->d_setup_status, c->d_q, c->d_u, c->d_l, c->d_x, c->d_y, c->d_rho, c->d_status, c->d_iter,
+                    c->d_xs, c->d_zs, c->d_ys, c->d_rhos, c->d_snx, c->d_sny, c->d_Fx, c->d_Fu, c->d_Fr,
+                    c->d_Sbar, c->d_Ku, c->d_W0, c->d_X, c->d_U};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
+    delete c;
+    return MPCQ_OK;
+}
+
+int mpcq_setup(mpcq_ctx *c, const double *P, const double *q0, const double *A, const double *l0,
+               const double *u0)
+{
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    const size_t Pn = c->dims.n_plants, n = c->dims.n, m = c->dims.m, B = c->dims.batch;
+    if (!P || !q0 || (m && (!A || !l0 || !u0))) return fail(MPCQ_ERR_ARG, "null setup array");
+    for (size_t i = 0; i < Pn * m; i++)
+        if (l0[i] > u0[i]) return fail(MPCQ_ERR_BOUNDS, "lower bound above upper bound (osqp validate_data)");
+    c->setup_done = false;
+    hipStream_t s = c->last;
+    if ((rc = h2d(c->d_P, P, 8 * Pn * n * n, s)) || (rc = h2d(c->d_q0, q0, 8 * Pn * n, s)) ||
+        (rc = h2d(c->d_A, A, 8 * Pn * m * n, s)) || (rc = h2d(c->d_l0, l0, 8 * Pn * m, s)) ||
+        (rc = h2d(c->d_u0, u0, 8 * Pn * m, s)))
+        return rc;
+    HIPCHK(hipMemsetAsync(c->d_ops, 0, 8 * Pn * c->ops_stride, s));
+    mpcq::SetupArgs a{};
+    a.n = (int)n;
+    a.m = (int)m;
+    a.nc = c->nc;
+    a.mc = c->mc;
+    a.n_plants = (int)Pn;
+    a.scaling = c->set.scaling;
+    a.sigma = c->set.sigma;
+    a.rho = c->set.rho;
+    a.P = c->d_P;
+    a.q0 = c->d_q0;
+    a.A = c->d_A;
+    a.l0 = c->d_l0;
+    a.u0 = c->d_u0;
+    a.ops = c->d_ops;
+    a.ctype = c->d_ctype;
+    a.scratch = c->d_scratch;
+    a.status = c->d_setup_status;
+    if (mpcq_internal_setup_launch(&a, s) != 0) return fail(MPCQ_ERR_HIP, "setup kernel launch failed");
+    std::vector<int> st(Pn), ct(Pn * c->mc);
+    HIPCHK(hipMemcpyAsync(st.data(), c->d_setup_status, 4 * Pn, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(ct.data(), c->d_ctype, 4 * Pn * c->mc, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (size_t p = 0; p < Pn; p++)
+        if (st[p] != 0) return fail(MPCQ_ERR_SETUP, "setup: P + sigma I not positive definite (non-convex QP)");
+    c->all_ineq = std::all_of(ct.begin(), ct.end(), [](int t) { return t == 0; });
+    if (c->dims.dtype == MPCQ_F32 &&
+        mpcq_internal_f64_to_f32(c->d_ops, c->d_ops32, Pn * c->ops_stride, s) != 0)
+        return fail(MPCQ_ERR_HIP, "operator conversion failed");
+    const int per = Pn > 1;
+    if (mpcq_internal_broadcast(c->d_q0, c->d_q, (int)n, (int)B, per, s) ||
+        mpcq_internal_broadcast(c->d_u0, c->d_u, (int)m, (int)B, per, s) ||
+        mpcq_internal_broadcast(c->d_l0, c->d_l, (int)m, (int)B, per, s))
+        return fail(MPCQ_ERR_HIP, "broadcast failed");
+    if ((rc = reset_state(c, true))) return rc;
+    // plant-0 scaling, for mpcq_get_scaling and host-side bound validation
+    const mpcq::OpsLayout L = mpcq::OpsLayout::make(c->nc, c->mc);
+    std::vector<double> blk(c->ops_stride);
+    HIPCHK(hipMemcpyAsync(blk.data(), c->d_ops, 8 * c->ops_stride, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (size_t i = 0; i < n; i++) c->hD[i] = blk[L.D + i];
+    for (size_t j = 0; j < m; j++) c->hE[j] = blk[L.E + j];
+    c->hc = blk[L.cs];
+    c->lower_free = lower_all_free(c, l0);
+    c->setup_done = true;
+    return MPCQ_OK;
+}
+
+int mpcq_update_lin_cost(mpcq_ctx *c, const double *q)
+{
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (!q) return fail(MPCQ_ERR_ARG, "null q");
+    return h2d(c->d_q, q, 8 * (size_t)c->dims.batch * c->dims.n, c->last);
+}
+
+int mpcq_update_upper_bound(mpcq_ctx *c, const double *u)
+{
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (!u) return fail(MPCQ_ERR_ARG, "null u");
+    return h2d(c->d_u, u, 8 * (size_t)c->dims.batch * c->dims.m, c->last);
+}
+
+int mpcq_update_lower_bound(mpcq_ctx *c, const double *l)
+{
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (!l) return fail(MPCQ_ERR_ARG, "null l");
+    c->lower_free = lower_all_free_batch(c, l);
+    return h2d(c->d_l, l, 8 * (size_t)c->dims.batch * c->dims.m, c->last);
+}
+
+int mpcq_update_bounds(mpcq_ctx *c, const double *l, const double *u)
+{
+    int rc = mpcq_update_lower_bound(c, l);
+    return rc ? rc : mpcq_update_upper_bound(c, u);
+}
+
+int mpcq_cold_start(mpcq_ctx *c)
+{
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if ((rc = reset_state(c, false))) return rc;
+    HIPCHK(hipStreamSynchronize(c->last));
+    return MPCQ_OK;
+}
+
+int mpcq_warm_start(mpcq_ctx *c, const double *x, const double *y)
+{
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (!x || (c->dims.m && !y)) return fail(MPCQ_ERR_ARG, "null x/y");
+    // stage in the output buffers (overwritten by the next solve)
+    if ((rc = h2d(c->d_x, x, 8 * (size_t)c->dims.batch * c->dims.n, c->last))) return rc;
+    if ((rc = h2d(c->d_y, y, 8 * (size_t)c->dims.batch * c->dims.m, c->last))) return rc;
+    if (c->dims.dtype == MPCQ_F32) {
+        auto a = make_args<float>(c);
+        rc = mpcq_internal_warm_f32(&a, c->nc, c->mc, c->d_x, c->d_y, c->last);
+    } else {
+        auto a = make_args<double>(c);
+        rc = mpcq_internal_warm_f64(&a, c->nc, c->mc, c->d_x, c->d_y, c->last);
+    }
+    if (rc) return fail(MPCQ_ERR_HIP, "warm start kernel failed");
+    HIPCHK(hipStreamSynchronize(c->last));
+    return MPCQ_OK;
+}
+
+static int launch_solve(mpcq_ctx *c, hipStream_t s, bool mpc, const double *X, double *U, double xref)
+{
+    int rc;
+    if (c->dims.dtype == MPCQ_F32) {
+        auto a = make_args<float>(c);
+        if (mpc) {
+            a.mpc = 1; a.nx = c->nx; a.X = X; a.U = U; a.xref = xref;
+            a.Fx = c->d_Fx; a.Fu = c->d_Fu; a.Fr = c->d_Fr; a.Sbar = c->d_Sbar; a.Ku = c->d_Ku; a.W0 = c->d_W0;
+            a.q_out = c->d_q; a.u_out = c->d_u;
+        }
+        rc = mpcq_internal_admm_launch_f32(&a, c->nc, c->mc, s);
+    } else {
+        auto a = make_args<double>(c);
+        if (mpc) {
+            a.mpc = 1; a.nx = c->nx; a.X = X; a.U = U; a.xref = xref;
+            a.Fx = c->d_Fx; a.Fu = c->d_Fu; a.Fr = c->d_Fr; a.Sbar = c->d_Sbar; a.Ku = c->d_Ku; a.W0 = c->d_W0;
+            a.q_out = c->d_q; a.u_out = c->d_u;
+        }
+        rc = mpcq_internal_admm_launch_f64(&a, c->nc, c->mc, s);
+    }
+    if (rc) return fail(MPCQ_ERR_HIP, std::string("ADMM kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    c->last = s;
+    c->fresh = false;
+    return MPCQ_OK;
+}
+
+int mpcq_reset(mpcq_ctx *c)
+{
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    c->fresh = true;
+    return MPCQ_OK;
+}
+
+int mpcq_solve(mpcq_ctx *c, void *stream)
+{
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    return launch_solve(c, (hipStream_t)stream, false, nullptr, nullptr, 0.0);
+}
+
+static int d2h(mpcq_ctx *c, void *dst, const void *src, size_t bytes)
+{
+    if (!dst || !bytes) return MPCQ_OK;
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->last));
+    HIPCHK(hipStreamSynchronize(c->last));
+    return MPCQ_OK;
+}
+
+int mpcq_get_solution(mpcq_ctx *c, double *x)
+{
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (!x) return fail(MPCQ_ERR_ARG, "null x");
+    return d2h(c, x, c->d_x, 8 * (size_t)c->dims.batch * c->dims.n);
+}
+
+int mpcq_get_dual(mpcq_ctx *c, double *y)
+{
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (!y && c->dims.m) return fail(MPCQ_ERR_ARG, "null y");
+    return d2h(c, y, c->d_y, 8 * (size_t)c->dims.batch * c->dims.m);
+}
+
+int mpcq_get_info(mpcq_ctx *c, int *status, int *iter, double *rho)
+{
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    const size_t B = c->dims.batch;
+    if ((rc = d2h(c, status, c->d_status, 4 * B))) return rc;
+    if ((rc = d2h(c, iter, c->d_iter, 4 * B))) return rc;
+    return d2h(c, rho, c->d_rho, 8 * B);
+}
+
+int mpcq_get_scaling(mpcq_ctx *c, double *D, double *E, double *cc)
+{
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (D) std::copy(c->hD.begin(), c->hD.end(), D);
+    if (E) std::copy(c->hE.begin(), c->hE.end(), E);
+    if (cc) *cc = c->hc;
+    return MPCQ_OK;
+}
+
+int mpcq_device_view_get(mpcq_ctx *c, mpcq_device_view *v)
+{
+    if (!c || !v) return fail(MPCQ_ERR_ARG, "null argument");
+    v->q = c->d_q;
+    v->u = c->d_u;
+    v->l = c->d_l;
+    v->x = c->d_x;
+    v->y = c->d_y;
+    v->status = c->d_status;
+    v->iter = c->d_iter;
+    v->rho = c->d_rho;
+    return MPCQ_OK;
+}
+
+int mpcq_mpc_set_operators(mpcq_ctx *c, int nx, const double *Fx, const double *Fu, const double *Fr,
+                           const double *Sbar, const double *Ku, const double *W0)
+{
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    const size_t Pn = c->dims.n_plants, n = c->dims.n, m = c->dims.m;
+    if (nx <= 0 || nx > 8) return fail(MPCQ_ERR_ARG, "nx must be in 1..8");
+    if (m != 2 * n) return fail(MPCQ_ERR_ARG, "MPC front end needs m == 2n (ModelPredictiveControlAPI.cpp:47-48)");
+    if (!Fx || !Fu || !Fr || !Sbar || !Ku || !W0) return fail(MPCQ_ERR_ARG, "null operator");
+    if (c->nx != nx) {
+        for (double **p : {&c->d_Fx, &c->d_Sbar})
+            if (*p) { (void)hipFree(*p); *p = nullptr; }
+    }
+    auto A = [&](double **p, size_t cnt) -> bool {
+        return *p || hipMalloc((void **)p, 8 * std::max<size_t>(cnt, 1)) == hipSuccess;
+    };
+    if (!A(&c->d_Fx, Pn * n * nx) || !A(&c->d_Fu, Pn * n) || !A(&c->d_Fr, Pn * n * n) ||
+        !A(&c->d_Sbar, Pn * m * nx) || !A(&c->d_Ku, Pn * m) || !A(&c->d_W0, Pn * m) ||
+        !A(&c->d_X, (size_t)c->dims.batch * 8) || !A(&c->d_U, (size_t)c->dims.batch))
+        return fail(MPCQ_ERR_HIP, "hipMalloc failed");
+    c->nx = nx;
+    hipStream_t s = c->last;
+    if ((rc = h2d(c->d_Fx, Fx, 8 * Pn * n * nx, s)) || (rc = h2d(c->d_Fu, Fu, 8 * Pn * n, s)) ||
+        (rc = h2d(c->d_Fr, Fr, 8 * Pn * n * n, s)) || (rc = h2d(c->d_Sbar, Sbar, 8 * Pn * m * nx, s)) ||
+        (rc = h2d(c->d_Ku, Ku, 8 * Pn * m, s)) || (rc = h2d(c->d_W0, W0, 8 * Pn * m, s)))
+        return rc;
+    c->mpc_ready = true;
+    return MPCQ_OK;
+}
+
+int mpcq_mpc_step_device(mpcq_ctx *c, const double *X, double *U, double xref, void *stream)
+{
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (!c->mpc_ready) return fail(MPCQ_ERR_ORDER, "mpcq_mpc_set_operators has not been called");
+    if (!X || !U) return fail(MPCQ_ERR_ARG, "null X/U");
+    return launch_solve(c, (hipStream_t)stream, true, X, U, xref);
+}
+
+int mpcq_mpc_step(mpcq_ctx *c, const double *X, double *U, double xref)
+{
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (!c->mpc_ready) return fail(MPCQ_ERR_ORDER, "mpcq_mpc_set_operators has not been called");
+    const size_t B = c->dims.batch;
+    if ((rc = h2d(c->d_X, X, 8 * B * c->nx, c->last)) || (rc = h2d(c->d_U, U, 8 * B, c->last))) return rc;
+    if ((rc = launch_solve(c, c->last, true, c->d_X, c->d_U, xref))) return rc;
+    return d2h(c, U, c->d_U, 8 * B);
+}
+
+int mpcq_condense(int device, int n_plants, int nx, int N, int s_rows, const double *Ad, const double *Bd,
+                  const double *Cd, const double *K, const double *Q, const double *R, const double *RD, double *P,
+                  double *A, double *Fx, double *Fu, double *Fr, double *Sbar, double *Ku, double *W0)
+{
+    if (n_plants <= 0 || nx <= 0 || nx > 8 || N <= 0 || s_rows < 0)
+        return fail(MPCQ_ERR_ARG, "condense: n_plants > 0, 1 <= nx <= 8, N > 0, s_rows >= 0");
+    const double *in[] = {Ad, Bd, Cd, K, Q, R, RD};
+    double *outp[] = {P, A, Fx, Fu, Fr, Sbar, Ku, W0};
+    for (auto p : in)
+        if (!p) return fail(MPCQ_ERR_ARG, "condense: null input");
+    for (auto p : outp)
+        if (!p) return fail(MPCQ_ERR_ARG, "condense: null output");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return fail(MPCQ_ERR_HIP, "no HIP device with this ordinal");
+    HIPCHK(hipSetDevice(device));
+    const size_t Pn = n_plants, X = nx, n = N;
+    const size_t in_cnt[] = {Pn * X * X, Pn * X, Pn * X, Pn * X, Pn, Pn, Pn};
+    const size_t out_cnt[] = {Pn * n * n, Pn * 2 * n * n, Pn * n * X, Pn * n, Pn * n * n, Pn * 2 * n * X, Pn * 2 * n, Pn * 2 * n};
+    const size_t scr = Pn * mpcq_internal_condense_scratch(nx, N);
+    size_t total = scr;
+    for (size_t c : in_cnt) total += c;
+    for (size_t c : out_cnt) total += c;
+    double *buf = nullptr;
+    HIPCHK(hipMalloc((void **)&buf, 8 * total));
+    mpcq::CondenseArgs a{};
+    double *p = buf;
+    const double **din[] = {&a.Ad, &a.Bd, &a.Cd, &a.K, &a.Q, &a.R, &a.RD};
+    double **dout[] = {&a.P, &a.A, &a.Fx, &a.Fu, &a.Fr, &a.Sbar, &a.Ku, &a.W0};
+    int rc = MPCQ_OK;
+    for (int i = 0; i < 7 && !rc; i++) {
+        *din[i] = p;
+        if (hipMemcpy(p, in[i], 8 * in_cnt[i], hipMemcpyHostToDevice) != hipSuccess) rc = fail(MPCQ_ERR_HIP, "h2d");
+        p += in_cnt[i];
+    }
+    for (int i = 0; i < 8; i++) {
+        *dout[i] = p;
+        p += out_cnt[i];
+    }
+    a.scratch = p;
+    a.n_plants = n_plants;
+    a.nx = nx;
+    a.N = N;
+    a.s_rows = s_rows;
+    if (!rc && mpcq_internal_condense_launch(&a, nullptr) != 0) rc = fail(MPCQ_ERR_HIP, "condense launch failed");
+    if (!rc && hipDeviceSynchronize() != hipSuccess) rc = fail(MPCQ_ERR_HIP, "condense kernel failed");
+    for (int i = 0; i < 8 && !rc; i++)
+        if (hipMemcpy(outp[i], *dout[i], 8 * out_cnt[i], hipMemcpyDeviceToHost) != hipSuccess)
+            rc = fail(MPCQ_ERR_HIP, "d2h");
+    (void)hipFree(buf);
+    return rc;
+}
+
+}  // extern "C"

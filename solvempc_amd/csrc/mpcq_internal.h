@@ -1,0 +1,167 @@
+// solvempc_amd/csrc/mpcq_internal.h — device data layout shared by the setup and ADMM kernels.
+//
+// Factorisation used on the device (replaces OSQP's QDLDL LDL' of the KKT matrix): for a plant
+// with scaled data (P^, A^) and constraint-type pattern s (rho_j = rho*s_j, or RHO_MIN for free
+// rows), the reduced KKT matrix is a one-parameter family
+//        M(rho) = P~ + rho G,   P~ = P^ + sigma I + RHO_MIN sum_free a_j a_j',  G = sum s_j a_j a_j'.
+// Setup computes the generalised eigen-basis  W' P~ W = I,  W' G W = diag(lambda), so that
+//        M(rho)^-1 = W diag(1/(1 + rho lambda)) W'
+// for EVERY rho.  An adaptive-rho update (OSQP adapt_rho) therefore only rescales a diagonal:
+// no refactorisation, and all QPs of a plant share W whatever rho each one has reached.
+// The ADMM iterate keeps x in that basis (x^ = W x'); see mpcq_admm.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace mpcq {
+
+// OSQP v0.6 constants (constants.h)
+constexpr double kInfty = 1e30;
+constexpr double kMinScaling = 1e-4;
+constexpr double kMaxScaling = 1e4;
+constexpr double kRhoMin = 1e-6;
+constexpr double kRhoMax = 1e6;
+constexpr double kRhoTol = 1e-4;
+constexpr double kRhoEqOverIneq = 1e3;
+constexpr double kDivisionTol = 1.0 / kInfty;
+
+// Per-plant operators, padded to the kernel capacity (NC variables, MC rows).  Row-major.
+// Every array is [n_plants][...]; padding entries are zero (padded rows: free, E = 1).
+template <typename T>
+struct PlantOps {
+    const T *lam;    // NC          generalised eigenvalues
+    const T *W;      // NC x NC     x^ = W x'
+    const T *sWtW;   // NC x NC     sigma * W'W   (the sigma x term of the KKT rhs, in W-basis)
+    const T *WtA;    // MC x NC     B = A^ W   (row j: b_j)
+    const T *PW;     // NC x NC     P^ W       (P x^ for the dual residual)
+    const T *Winv;   // NC x NC     W^-1 = V' L'  (osqp_warm_start: x' = W^-1 x^)
+    const T *Ah;     // MC x NC     A^         (A' y for the dual residual)
+    const T *D;      // NC          Ruiz D     (Dinv = 1/D)
+    const T *E;      // MC          Ruiz E
+    const T *Dinv;   // NC
+    const T *Einv;   // MC
+    const T *cs;     // 2           c, 1/c
+    const T *rscale; // MC          rho_j = rho * rscale_j  (0 => free row => RHO_MIN)
+    const int *ctype;// MC          OSQP constr_type: -1 free, 0 inequality, 1 equality
+};
+
+// Shapes of one plant's operator block, in elements, for capacities (nc, mc).
+struct OpsLayout {
+    int nc, mc;
+    size_t lam, W, sWtW, WtA, PW, Winv, Ah, D, E, Dinv, Einv, cs, rscale, total;
+    __host__ __device__ static constexpr OpsLayout make(int nc, int mc)
+    {
+        OpsLayout L{};
+        L.nc = nc;
+        L.mc = mc;
+        size_t o = 0;
+        L.lam = o; o += nc;
+        L.W = o; o += (size_t)nc * nc;
+        L.sWtW = o; o += (size_t)nc * nc;
+        L.WtA = o; o += (size_t)mc * nc;
+        L.PW = o; o += (size_t)nc * nc;
+        L.Winv = o; o += (size_t)nc * nc;
+        L.Ah = o; o += (size_t)mc * nc;
+        L.D = o; o += nc;
+        L.E = o; o += mc;
+        L.Dinv = o; o += nc;
+        L.Einv = o; o += mc;
+        L.cs = o; o += 2;
+        L.rscale = o; o += mc;
+        L.total = o;
+        return L;
+    }
+};
+
+struct SolverSettings {
+    double rho, sigma, alpha;
+    double eps_abs, eps_rel, eps_prim_inf, eps_dual_inf;
+    double adaptive_rho_tolerance;
+    int max_iter, check_termination, adaptive_rho, adaptive_rho_interval;
+    int warm_start, scaled_termination, scaling;
+};
+
+// Status values (mirror include/mpcq.h)
+enum : int {
+    kSolved = 1,
+    kSolvedInaccurate = 2,
+    kPrimalInfeasibleInaccurate = 3,
+    kDualInfeasibleInaccurate = 4,
+    kMaxIterReached = -2,
+    kPrimalInfeasible = -3,
+    kDualInfeasible = -4,
+    kNonCvx = -7,
+    kUnsolved = -10,
+    kInvalidBounds = -20,
+    kTypeChanged = -21,
+};
+
+// Arguments of the setup kernel (one 64-lane workgroup per plant).
+struct SetupArgs {
+    int n, m, nc, mc, n_plants;
+    int scaling;       // Ruiz passes
+    double sigma, rho;
+    const double *P, *q0, *A, *l0, *u0;  // [plant] n*n, n, m*n, m, m
+    double *ops;       // [plant] OpsLayout(nc, mc).total
+    int *ctype;        // [plant] mc
+    double *scratch;   // [plant] scratch_len(n, m)
+    int *status;       // [plant] 0 ok, else error
+};
+
+// Arguments of the ADMM kernel (one QP per lane).
+template <typename T>
+struct AdmmArgs {
+    int batch, n, m;
+    int shared;                 // 1: every QP uses plant 0
+    size_t ops_stride;          // elements per plant block (OpsLayout::total)
+    PlantOps<T> ops;
+    const int *ctype;           // [plant][mc]
+    SolverSettings st;
+    int adaptive_interval;      // resolved (0 -> 4*check_termination)
+    int all_ineq;               // every row of every plant is an inequality (constr_type 0)
+    int lower_free;             // every l^ of every QP is below -OSQP_INFTY*MIN_SCALING
+    // per-QP inputs (fp64, QP-major as in the C ABI)
+    const double *q, *u, *l;    // batch*n, batch*m, batch*m (l may be a single shared m-vector)
+    int l_shared;
+    // state (SoA [row][batch], T) for warm start
+    T *xs, *zs, *ys, *rhos;
+    int warm;                   // read xs/zs/ys at entry (settings.warm_start)
+    int fresh;                  // ignore stored state: x = z = y = 0, rho = settings.rho (mpcq_reset)
+    // snapshots for the infeasibility certificates (SoA)
+    T *snap_x, *snap_y;
+    // outputs
+    double *x, *y, *rho_out;
+    int *status, *iter;
+    // MPC front end (n = N, m = 2N); null when unused
+    int mpc, nx;
+    const double *X, *Fx, *Fu, *Fr, *Sbar, *Ku, *W0;
+    double *U, *q_out, *u_out;
+    double xref;
+};
+
+}  // namespace mpcq
+
+namespace mpcq {
+struct CondenseArgs {
+    int n_plants, nx, N, s_rows;
+    const double *Ad, *Bd, *Cd, *K, *Q, *R, *RD;  // [plant] nx*nx, nx, nx, nx, 1, 1, 1
+    double *P, *A, *Fx, *Fu, *Fr, *Sbar, *Ku, *W0;  // [plant] N*N, 2N*N, N*nx, N, N*N, 2N*nx, 2N, 2N
+    double *scratch;                                 // [plant] condense_scratch_len
+};
+}  // namespace mpcq
+
+// Launchers (extern "C" so the host library links them without templates).
+extern "C" {
+int mpcq_internal_setup_launch(const mpcq::SetupArgs *args, hipStream_t stream);
+int mpcq_internal_f64_to_f32(const double *in, float *out, size_t count, hipStream_t s);
+int mpcq_internal_broadcast(const double *src, double *dst, int len, int batch, int per_qp_src, hipStream_t s);
+int mpcq_internal_fill(void *p, int is_f32, double v, size_t count, hipStream_t s);
+int mpcq_internal_caps(int n, int m, int *nc, int *mc);
+int mpcq_internal_condense_launch(const mpcq::CondenseArgs *a, hipStream_t s);
+size_t mpcq_internal_condense_scratch(int nx, int N);
+int mpcq_internal_admm_launch_f64(const mpcq::AdmmArgs<double> *a, int nc, int mc, hipStream_t s);
+int mpcq_internal_admm_launch_f32(const mpcq::AdmmArgs<float> *a, int nc, int mc, hipStream_t s);
+int mpcq_internal_warm_f64(const mpcq::AdmmArgs<double> *a, int nc, int mc, const double *x, const double *y,
+                           hipStream_t s);
+int mpcq_internal_warm_f32(const mpcq::AdmmArgs<float> *a, int nc, int mc, const double *x, const double *y,
+                           hipStream_t s);
+}

@@ -1,0 +1,23 @@
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a gfx950 (MI355X) device; run with -m gpu")
+
+
+@pytest.fixture(scope="session")
+def plant():
+    from solvempc_amd import workload
+
+    return workload.reference_plant()
+
+
+@pytest.fixture(scope="session")
+def golden_dir():
+    return ROOT / "tests" / "golden"

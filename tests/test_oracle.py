@@ -1,0 +1,126 @@
+"""CPU tests of the checker itself (oracle/): pinned against the reference's known-answer values
+(produced by a survey-time build of /root/reference's own
+ModelPredictiveControlAPI.cpp) and certified by KKT conditions where no reference output exists."""
+import numpy as np
+import pytest
+
+import oracle
+from solvempc_amd import workload
+
+LMIN = -np.finfo(np.float64).max
+
+
+def test_condense_known_answers(plant):
+    """SURVEY.md Appendix B KATs (N = 15, the reference's mpcWindow)."""
+    o = oracle.condense(plant, 15)
+    kat = {
+        ("P", 0, 0): 11.000054467922261, ("P", 0, 1): 0.93338663476976957,
+        ("P", 14, 14): 10.066666709654967, ("P", 0, 14): 0.066666845462466012,
+        ("Fu", 0): 0.066721134682260722, ("Fu", 14): 0.066666845462466012,
+        ("Su", 0, 0): -0.000112452562885, ("Su", 1, 0): -0.00035904021540417532,
+    }
+    for (name, *idx), v in kat.items():
+        assert o[name][tuple(idx)] == pytest.approx(v, rel=1e-13, abs=1e-18), (name, idx)
+    np.testing.assert_allclose(o["Fx"][0], [-0.048643271265083346, -0.0063463657998492186,
+                                            0.01008331963724376, 0.0011545376299916823], rtol=1e-13)
+    ev = np.linalg.eigvalsh(o["P"])
+    assert ev[0] == pytest.approx(10.0168, abs=1e-4) and ev[-1] == pytest.approx(16.4972, abs=1e-4)
+    L = np.tril(np.ones((15, 15)))
+    np.testing.assert_array_equal(o["A"], np.vstack([-50 * L, 50 * L]))
+    X = np.array([0.01, 0.0, 0.02, 0.0])
+    u = oracle.upper_bound(o, X, 0.0)
+    np.testing.assert_allclose(u, [364.5] * 10 + [255] * 5 + [145.5] * 10 + [255] * 5, rtol=1e-15)
+    q = oracle.gradient(o, X, 0.0)
+    assert q[0] == pytest.approx(-0.00028476631990595827, rel=1e-13)
+    assert q[14] == pytest.approx(-1.5216160607417957e-06, rel=1e-12)
+    o20 = oracle.condense(plant, 20)
+    ev = np.linalg.eigvalsh(o20["P"])
+    assert ev[0] == pytest.approx(10.0168, abs=1e-4) and ev[-1] == pytest.approx(21.3607, abs=1e-4)
+    # S rows >= 10 are never written by the reference (:185) => zero; Sbar nonzero rows 0-9, 20-29
+    nz = np.nonzero(np.abs(o20["Sbar"]).sum(axis=1))[0]
+    np.testing.assert_array_equal(nz, list(range(10)) + list(range(20, 30)))
+
+
+def test_quirks(plant):
+    """Appendix A: Su strict upper triangle zero; Fu uses diag(LL' Rbar') = R (not LL' Rbar 1)."""
+    o = oracle.condense(plant, 15)
+    assert np.all(np.triu(o["Su"], 1) == 0)
+    Q, R = plant["Q"], plant["R"]
+    np.testing.assert_allclose(o["Fu"], 2 * (R + Q * o["Su"][:, 0] @ o["Su"]), rtol=1e-14)
+
+
+@pytest.mark.parametrize("N", [15, 20])
+def test_golden_regression(golden_dir, plant, N):
+    """The oracle still reproduces the committed fixtures (tests/golden/make_golden.py)."""
+    g = np.load(golden_dir / f"qp_n{N}.npz", allow_pickle=False)
+    o = oracle.condense(plant, N)
+    for k in ("P", "A", "Fx", "Fu", "Fr", "Sbar", "Ku", "W0"):
+        np.testing.assert_allclose(o[k], g[k], rtol=1e-15, atol=0, err_msg=k)
+    np.testing.assert_allclose(oracle.gradient(o, g["X"], g["U"]), g["q"], rtol=1e-14, atol=1e-300)
+    x, st, it, rho = oracle.batch_solve(o["P"], o["A"], np.zeros(N), np.full(2 * N, LMIN),
+                                        oracle.upper_bound(o, np.zeros(4), 0.0), g["q"], g["u"], nthreads=1)
+    np.testing.assert_array_equal(st, g["status"])
+    np.testing.assert_array_equal(it, g["iter"])
+    np.testing.assert_allclose(x, g["x"], rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("N", [15, 20])
+def test_tight_solution_is_kkt_optimal(golden_dir, plant, N):
+    """Optimum mode: at eps 1e-10 the restatement satisfies KKT (independent of OSQP)."""
+    g = np.load(golden_dir / f"qp_n{N}.npz", allow_pickle=False)
+    o = oracle.condense(plant, N)
+    l = np.full(2 * N, LMIN)
+    s = oracle.Solver(o["P"], np.zeros(N), o["A"], l, oracle.upper_bound(o, np.zeros(4), 0.0),
+                      oracle.default_settings(eps_abs=1e-10, eps_rel=1e-10, max_iter=200000))
+    for b in range(0, 64, 8):
+        assert s.update_gradient(g["q"][b]) and s.update_upper_bound(g["u"][b])
+        assert s.solve() == oracle.SOLVED
+        r = oracle.kkt_residuals(o["P"], g["q"][b], o["A"], l, g["u"][b], s.x(), s.y())
+        scale = 1 + np.abs(g["q"][b]).max() + np.abs(o["A"].T @ s.y()).max()
+        assert r["stationarity"] < 1e-7 * scale and r["primal"] < 1e-7 * (1 + np.abs(g["u"][b]).max())
+        assert r["dual_sign"] < 1e-12 * scale and r["complementarity"] < 1e-5 * scale
+        np.testing.assert_allclose(s.x(), g["x_opt"][b], atol=1e-6)
+    # default-eps answers are close to, but not at, the optimum
+    assert np.abs(g["x"] - g["x_opt"]).max() < 0.2
+
+
+def test_osqp_scaling_and_defaults(plant):
+    o = oracle.condense(plant, 20)
+    s = oracle.Solver(o["P"], np.zeros(20), o["A"], np.full(40, LMIN), oracle.upper_bound(o, np.zeros(4), 0.0))
+    D, E, c = s.scaling()
+    np.testing.assert_allclose(D, 1 / np.sqrt(50), rtol=1e-14)  # A entries +-50 dominate Ruiz
+    np.testing.assert_allclose(E, 1 / np.sqrt(50), rtol=1e-14)
+    assert c == 1.0  # q == 0 at setup => cost scaling limited to 1 (scaling.c)
+    st = oracle.default_settings()
+    assert (st.rho, st.sigma, st.alpha, st.max_iter, st.check_termination, st.scaling) == (0.1, 1e-6, 1.6, 4000, 25, 10)
+
+
+def test_infeasibility_statuses():
+    P = np.eye(2)
+    A = np.array([[1.0, 0.0], [1.0, 0.0]])
+    s = oracle.Solver(P, np.zeros(2), A, np.array([-1e30, 1.0]), np.array([-1.0, 1e30]))
+    assert s.solve() == oracle.PRIMAL_INFEASIBLE
+    assert np.all(np.isnan(s.x()))
+    # dual infeasible: P = 0 (PSD), q = (-1, 0), x0 unbounded above
+    s = oracle.Solver(np.zeros((2, 2)), np.array([-1.0, 0.0]), np.array([[0.0, 1.0]]), np.array([-1.0]), np.array([1.0]))
+    assert s.solve() == oracle.DUAL_INFEASIBLE
+
+
+def test_max_iter_and_warm_start(plant):
+    o = oracle.condense(plant, 20)
+    X, U = workload.mpc_states(1, 0, 1)
+    q, u = oracle.gradient(o, X, U)[0], oracle.upper_bound(o, X, U)[0]
+    l = np.full(40, LMIN)
+    s = oracle.Solver(o["P"], np.zeros(20), o["A"], l, oracle.upper_bound(o, np.zeros(4), 0.0),
+                      oracle.default_settings(max_iter=10, eps_abs=1e-12, eps_rel=1e-12))
+    s.update_gradient(q)
+    s.update_upper_bound(u)
+    assert s.solve() == oracle.MAX_ITER_REACHED and s.info().iter == 10
+    # warm start: a second solve of the same data converges in one check interval
+    s2 = oracle.Solver(o["P"], np.zeros(20), o["A"], l, oracle.upper_bound(o, np.zeros(4), 0.0))
+    s2.update_gradient(q)
+    s2.update_upper_bound(u)
+    assert s2.solve() == oracle.SOLVED
+    s2.update_gradient(q)
+    s2.update_upper_bound(u)
+    assert s2.solve() == oracle.SOLVED and s2.info().iter == 25
