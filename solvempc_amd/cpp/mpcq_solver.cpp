@@ -1,0 +1,149 @@
+// solvempc_amd/cpp/mpcq_solver.cpp — osqp-eigen-shaped single-QP solver over the C ABI.
+#include "mpcq_solver.hpp"
+
+#include <cstdio>
+
+namespace mpcq {
+
+std::vector<double> Matrix::row_major() const
+{
+    std::vector<double> out((size_t)r_ * c_);
+    for (int i = 0; i < r_; i++)
+        for (int j = 0; j < c_; j++) out[(size_t)i * c_ + j] = (*this)(i, j);
+    return out;
+}
+
+Matrix Matrix::from_row_major(int rows, int cols, const double *p)
+{
+    Matrix m(rows, cols);
+    for (int i = 0; i < rows; i++)
+        for (int j = 0; j < cols; j++) m(i, j) = p[(size_t)i * cols + j];
+    return m;
+}
+
+// osqp-eigen's Data setters check the sizes against setNumberOf* and return false on mismatch.
+bool Solver::Data::setHessianMatrix(const Matrix &H)
+{
+    if (n_ < 0 || H.rows() != n_ || H.cols() != n_) return false;
+    P_ = H;
+    hasP_ = true;
+    return true;
+}
+
+bool Solver::Data::setGradient(const Vector &q)
+{
+    if (n_ < 0 || (int)q.size() != n_) return false;
+    q_ = q;
+    hasQ_ = true;
+    return true;
+}
+
+bool Solver::Data::setLinearConstraintsMatrix(const Matrix &A)
+{
+    if (n_ < 0 || m_ < 0 || A.rows() != m_ || A.cols() != n_) return false;
+    A_ = A;
+    hasA_ = true;
+    return true;
+}
+
+bool Solver::Data::setLowerBound(const Vector &l)
+{
+    if (m_ < 0 || (int)l.size() != m_) return false;
+    l_ = l;
+    hasL_ = true;
+    return true;
+}
+
+bool Solver::Data::setUpperBound(const Vector &u)
+{
+    if (m_ < 0 || (int)u.size() != m_) return false;
+    u_ = u;
+    hasU_ = true;
+    return true;
+}
+
+Solver::~Solver() { clearSolver(); }
+
+void Solver::clearSolver()
+{
+    if (ctx_) mpcq_destroy(ctx_);
+    ctx_ = nullptr;
+}
+
+bool Solver::fail(const char *where)
+{
+    err_ = std::string(where) + ": " + mpcq_last_error();
+    if (settings_.raw().verbose) std::fprintf(stderr, "[mpcq::Solver] %s\n", err_.c_str());
+    return false;
+}
+
+bool Solver::initSolver()
+{
+    if (ctx_) return fail("initSolver: already initialised");
+    const Data &d = data_;
+    if (!(d.hasP_ && d.hasQ_ && d.hasA_ && d.hasL_ && d.hasU_)) return fail("initSolver: data not set");
+    mpcq_dims dims{d.n_, d.m_, 1, 1, MPCQ_F64, device_};
+    if (mpcq_create(&dims, &settings_.raw(), &ctx_) != MPCQ_OK) {
+        ctx_ = nullptr;
+        return fail("mpcq_create");
+    }
+    const std::vector<double> P = d.P_.row_major(), A = d.A_.row_major();
+    if (mpcq_setup(ctx_, P.data(), d.q_.data(), A.data(), d.l_.data(), d.u_.data()) != MPCQ_OK) {
+        fail("mpcq_setup");
+        clearSolver();
+        return false;
+    }
+    E_.assign(d.m_, 1.0);
+    std::vector<double> D(d.n_);
+    double c = 1.0;
+    mpcq_get_scaling(ctx_, D.data(), E_.data(), &c);
+    l_scaled_.resize(d.m_);
+    for (int i = 0; i < d.m_; i++) l_scaled_[i] = d.l_[i] * E_[i];
+    x_.assign(d.n_, 0.0);
+    y_.assign(d.m_, 0.0);
+    return true;
+}
+
+bool Solver::updateGradient(const Vector &q)
+{
+    if (!ctx_ || (int)q.size() != data_.n_) return fail("updateGradient");
+    return mpcq_update_lin_cost(ctx_, q.data()) == MPCQ_OK || fail("mpcq_update_lin_cost");
+}
+
+bool Solver::updateUpperBound(const Vector &u)
+{
+    if (!ctx_ || (int)u.size() != data_.m_) return fail("updateUpperBound");
+    for (int i = 0; i < data_.m_; i++)  // osqp_update_upper_bound: scaled u must not be below scaled l
+        if (u[i] * E_[i] < l_scaled_[i]) return fail("updateUpperBound: upper bound below lower bound");
+    return mpcq_update_upper_bound(ctx_, u.data()) == MPCQ_OK || fail("mpcq_update_upper_bound");
+}
+
+bool Solver::updateLowerBound(const Vector &l)
+{
+    if (!ctx_ || (int)l.size() != data_.m_) return fail("updateLowerBound");
+    if (mpcq_update_lower_bound(ctx_, l.data()) != MPCQ_OK) return fail("mpcq_update_lower_bound");
+    for (int i = 0; i < data_.m_; i++) l_scaled_[i] = l[i] * E_[i];
+    return true;
+}
+
+bool Solver::updateBounds(const Vector &l, const Vector &u)
+{
+    if (!ctx_ || (int)l.size() != data_.m_ || (int)u.size() != data_.m_) return fail("updateBounds");
+    for (int i = 0; i < data_.m_; i++)
+        if (l[i] > u[i]) return fail("updateBounds: lower bound above upper bound");
+    if (mpcq_update_bounds(ctx_, l.data(), u.data()) != MPCQ_OK) return fail("mpcq_update_bounds");
+    for (int i = 0; i < data_.m_; i++) l_scaled_[i] = l[i] * E_[i];
+    return true;
+}
+
+bool Solver::solve()
+{
+    if (!ctx_) return fail("solve: solver not initialised");
+    if (mpcq_solve(ctx_, nullptr) != MPCQ_OK) return fail("mpcq_solve");
+    if (mpcq_get_info(ctx_, &status_, &iter_, &rho_) != MPCQ_OK) return fail("mpcq_get_info");
+    if (mpcq_get_solution(ctx_, x_.data()) != MPCQ_OK) return fail("mpcq_get_solution");
+    if (data_.m_ > 0 && mpcq_get_dual(ctx_, y_.data()) != MPCQ_OK) return fail("mpcq_get_dual");
+    return status_ == MPCQ_SOLVED;
+}
+
+}  // namespace mpcq

@@ -46,7 +46,7 @@ __device__ bool primal_infeasible(const AdmmArgs<T> &a, const PlantOps<T> &op, c
     // lh == nullptr: every lower bound is -inf (LFREE kernel variant)
     const size_t B = a.batch;
     auto dyj = [&](int j) -> T {  // delta_y projected onto the polar of the recession cone of [l,u]
-        T d = a.ys[j * B + b] - a.snap_y[j * B + b];
+        T d = a.ys[b * MC + j] - a.snap_y[b * MC + j];
         const T up = uh[j * 64], lo = lh ? lh[j * 64] : T(-kInfty);
         const bool uinf = up > T(kInfty * kMinScaling), linf = lo < T(-kInfty * kMinScaling);
         if (uinf) d = linf ? T(0) : tmin(d, T(0));
@@ -80,7 +80,7 @@ __device__ bool dual_infeasible(const AdmmArgs<T> &a, const PlantOps<T> &op, con
                                 const T *uh, const T *lh, int b, T eps, bool scaled)
 {
     const size_t B = a.batch;
-    auto dxp = [&](int k) -> T { return a.xs[k * B + b] - a.snap_x[k * B + b]; };
+    auto dxp = [&](int k) -> T { return a.xs[b * NC + k] - a.snap_x[b * NC + k]; };
     T qdx = 0;  // q^' dx^ = (W' q^)' dx'
 #pragma unroll 1
     for (int k = 0; k < NC; k++) qdx = tfma(g[k * 64], dxp(k), qdx);
@@ -143,8 +143,14 @@ struct LdsLayout {
     static constexpr int total = (2 * NC + MC + (LFREE ? 0 : MC)) * 64;
 };
 
+// Register budget: the per-lane iterate is (NC + 2 MC) values (+ NC temporaries); ask for the
+// occupancy that budget allows (fp32: 3 waves/SIMD <= 168 VGPRs, fp64: 2 waves/SIMD <= 256),
+// otherwise the scheduler spends registers on ILP up to the 512 a 64-lane block permits.
+template <typename T> constexpr int kWavesPerSimd = sizeof(T) == 4 ? 3 : 2;
+
 template <typename T, int NC, int MC, bool SHARED, bool ALL_INEQ, bool LFREE>
-__global__ __launch_bounds__(64) void admm_lane_kernel(AdmmArgs<T> a)
+__global__ __launch_bounds__(64) 
+void admm_lane_kernel(AdmmArgs<T> a)
 {
     constexpr OpsLayout L = OpsLayout::make(NC, MC);
     using LL = LdsLayout<T, NC, MC, LFREE>;
@@ -245,9 +251,9 @@ __global__ __launch_bounds__(64) void admm_lane_kernel(AdmmArgs<T> a)
     T rho = a.fresh ? (T)fmin(fmax(st.rho, kRhoMin), kRhoMax) : a.rhos[b];
     if (a.warm && !a.fresh) {
 #pragma unroll
-        for (int k = 0; k < NC; k++) xs[k] = a.xs[k * B + b];
+        for (int k = 0; k < NC; k++) xs[k] = a.xs[b * NC + k];
 #pragma unroll
-        for (int j = 0; j < MC; j++) { z[j] = a.zs[j * B + b]; y[j] = a.ys[j * B + b]; }
+        for (int j = 0; j < MC; j++) { z[j] = a.zs[b * MC + j]; y[j] = a.ys[b * MC + j]; }
     } else {
 #pragma unroll
         for (int k = 0; k < NC; k++) xs[k] = 0;
@@ -269,9 +275,9 @@ __global__ __launch_bounds__(64) void admm_lane_kernel(AdmmArgs<T> a)
             const bool info = at_check || at_adapt || last;
             if (info) {  // snapshot x', y: the certificates use this iteration's delta_x, delta_y
 #pragma unroll
-                for (int k = 0; k < NC; k++) a.snap_x[k * B + b] = xs[k];
+                for (int k = 0; k < NC; k++) a.snap_x[b * NC + k] = xs[k];
 #pragma unroll
-                for (int j = 0; j < MC; j++) a.snap_y[j * B + b] = y[j];
+                for (int j = 0; j < MC; j++) a.snap_y[b * MC + j] = y[j];
             }
             // ---- xi = -g + sigma W'W x' + B' w,   w_j = rho_j z_j - y_j
             T xi[NC];
@@ -380,7 +386,7 @@ __global__ __launch_bounds__(64) void admm_lane_kernel(AdmmArgs<T> a)
                         prim_ok = true;
                     } else {
 #pragma unroll
-                        for (int j = 0; j < MC; j++) a.ys[j * B + b] = y[j];
+                        for (int j = 0; j < MC; j++) a.ys[b * MC + j] = y[j];
                         prim_inf = primal_infeasible<T, NC, MC>(a, op, uh, LFREE ? nullptr : lh, b,
                                                                 (T)st.eps_prim_inf * mul, scaled_term);
                     }
@@ -391,7 +397,7 @@ __global__ __launch_bounds__(64) void admm_lane_kernel(AdmmArgs<T> a)
                     dual_ok = true;
                 } else {
 #pragma unroll
-                    for (int k = 0; k < NC; k++) a.xs[k * B + b] = xs[k];
+                    for (int k = 0; k < NC; k++) a.xs[b * NC + k] = xs[k];
                     dual_inf = dual_infeasible<T, NC, MC>(a, op, g, uh, LFREE ? nullptr : lh, b,
                                                           (T)st.eps_dual_inf * mul, scaled_term);
                 }
@@ -450,11 +456,11 @@ __global__ __launch_bounds__(64) void admm_lane_kernel(AdmmArgs<T> a)
     }
     const bool keep = has_sol || status == kInvalidBounds || status == kTypeChanged;
 #pragma unroll
-    for (int k = 0; k < NC; k++) a.xs[k * B + b] = keep ? xs[k] : T(0);
+    for (int k = 0; k < NC; k++) a.xs[b * NC + k] = keep ? xs[k] : T(0);
 #pragma unroll
     for (int j = 0; j < MC; j++) {
-        a.zs[j * B + b] = keep ? z[j] : T(0);
-        a.ys[j * B + b] = keep ? y[j] : T(0);
+        a.zs[b * MC + j] = keep ? z[j] : T(0);
+        a.ys[b * MC + j] = keep ? y[j] : T(0);
     }
     a.rhos[b] = rho;
     a.status[b] = status;
@@ -479,15 +485,15 @@ __global__ __launch_bounds__(64) void warm_start_kernel(AdmmArgs<T> a, const dou
         T s = 0;
         #pragma unroll
         for (int i = 0; i < NC; i++) s = tfma(op.Winv[po + k * NC + i], xh[i], s);
-        a.xs[(size_t)k * B + b] = s;
+        a.xs[(size_t)b * NC + k] = s;
     }
     #pragma unroll
     for (int j = 0; j < MC; j++) {
         T s = 0;
         #pragma unroll
         for (int k = 0; k < NC; k++) s = tfma(op.Ah[po + j * NC + k], xh[k], s);
-        a.zs[(size_t)j * B + b] = s;
-        a.ys[(size_t)j * B + b] =
+        a.zs[(size_t)b * MC + j] = s;
+        a.ys[(size_t)b * MC + j] =
             j < m ? (T)((y[(size_t)b * m + j] * (double)op.Einv[po + j]) * (double)op.cs[po]) : T(0);
     }
 }

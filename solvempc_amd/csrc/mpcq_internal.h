@@ -122,11 +122,11 @@ struct AdmmArgs {
     // per-QP inputs (fp64, QP-major as in the C ABI)
     const double *q, *u, *l;    // batch*n, batch*m, batch*m (l may be a single shared m-vector)
     int l_shared;
-    // state (SoA [row][batch], T) for warm start
+    // state (QP-major [batch][row], T) for warm start
     T *xs, *zs, *ys, *rhos;
     int warm;                   // read xs/zs/ys at entry (settings.warm_start)
     int fresh;                  // ignore stored state: x = z = y = 0, rho = settings.rho (mpcq_reset)
-    // snapshots for the infeasibility certificates (SoA)
+    // snapshots for the infeasibility certificates (QP-major)
     T *snap_x, *snap_y;
     // outputs
     double *x, *y, *rho_out;

@@ -1,7 +1,9 @@
 """GPU parity tests: the HIP path through the C ABI vs the CPU oracle (oracle/), same seeded inputs.
 
-Bar: fp64 kernel == oracle trajectory (same status, same iteration count, |dx| <= 1e-9 abs); the
-fp32 kernel within 1e-5 on the applied move and the same status.  Full-size (65,536 QP) runs are
+Bar: fp64 kernel == oracle trajectory (same status, same iteration count, |dx| <= 1e-9 abs), i.e.
+far inside the north-star bound ||u* - u*_osqp||_inf < 1e-5.  The fp32 kernel is held to
+1e-5 * max(1, |x|) (fp32 carries ~7 significant digits; moves reach |x0| ~ 40) on QPs that follow the
+oracle's iteration schedule, and >= 97% of QPs must follow it.  Full-size (65,536 QP) runs are
 checked through size-independent properties (KKT residuals at the solver's own tolerance).
 """
 import numpy as np
@@ -64,7 +66,8 @@ def test_fp32_parity(plant):
     same = it == it_ref
     assert same.mean() > 0.97, f"iteration schedule matches oracle on {same.mean():.3%}"
     # applied move (ModelPredictiveControlAPI.cpp:105) on QPs with the oracle's schedule
-    assert np.abs(x[same, 0] - x_ref[same, 0]).max() < 1e-5
+    err0 = np.abs(x[same, 0] - x_ref[same, 0]) / np.maximum(1.0, np.abs(x_ref[same, 0]))
+    assert err0.max() < 1e-5
     rel = np.abs(x[same] - x_ref[same]).max(axis=1) / np.maximum(1.0, np.abs(x_ref[same]).max(axis=1))
     assert rel.max() < 1e-5
 
@@ -196,8 +199,10 @@ def test_full_batch_kkt_properties(plant):
     prim = np.maximum(Ax - u, 0).max(axis=1)
     tol_p = 1e-3 + 1e-3 * np.maximum(np.abs(Ax).max(axis=1), np.abs(u).max(axis=1))
     assert np.all(prim <= 1.5 * tol_p)
-    dual = np.abs(x @ ops["P"] + q + y @ ops["A"]).max(axis=1)
-    assert np.all(dual < 1e-2 * np.maximum(1, np.abs(q).max(axis=1)) + 1e-3)
+    Px, Aty = x @ ops["P"], y @ ops["A"]
+    dual = np.abs(Px + q + Aty).max(axis=1)
+    tol_d = 1e-3 + 1e-3 * np.maximum(np.abs(q).max(axis=1), np.maximum(np.abs(Aty).max(axis=1), np.abs(Px).max(axis=1)))
+    assert np.all(dual <= 1.5 * tol_d)
     # shard invariance: the first 4096 QPs equal the oracle-parity run above
     x_ref, st_ref, it_ref, _ = _oracle_solve(ops, q[:1024], u[:1024], N)
     assert np.array_equal(it[:1024], it_ref) and np.abs(x[:1024] - x_ref).max() < 1e-9
