@@ -17,7 +17,7 @@ for dt in ${BENCH_DTYPES:-f32 f64}; do
 done
 if [ -n "$PROFILE" ]; then
   for dt in ${BENCH_DTYPES:-f32 f64}; do
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$dt -o run -- python bench.py --steps 5 --warmup 1 --dtype $dt --cpu-seconds 0 > gpurun_out/prof_$dt.log 2>&1
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$dt -o run -- python bench.py --steps 5 --warmup 1 --dtype $dt --cpu-seconds 0 > gpurun_out/prof_$dt.log 2>&1
     rc=$?; if [ $rc -ne 0 ]; then echo "rocprof $dt rc=$rc" >> gpurun_out/prof_$dt.log; exit $rc; fi
   done
 fi

@@ -1,4 +1,4 @@
-// solvempc_amd/csrc/mpcq_admm.hip — the hot path: batched OSQP-v0.6 ADMM on gfx950.
+// solvempc_amd/csrc/mpcq_admm.h — the per-plant path: batched OSQP-v0.6 ADMM on gfx950.
 //
 // Replaces osqp_solve behind OsqpEigen::Solver::solve (ModelPredictiveControlAPI.cpp:102), plus the
 // per-step updates around it (updateGradient :96 -> osqp_update_lin_cost, updateUpperBound :99 ->
@@ -21,6 +21,7 @@
 //   z_j    = Pi_[l,u](alpha zt_j + (1-alpha) z_j + y_j/rho_j)  (update_z)
 //   y_j   += rho_j (alpha zt_j + (1-alpha) z_j_prev - z_j)     (update_y)
 // every check_termination iterations: OSQP update_info / check_termination / adapt_rho.
+#pragma once
 #include "mpcq_internal.h"
 
 #include <math.h>
@@ -447,7 +448,7 @@ void admm_lane_kernel(AdmmArgs<T> a)
             v = __builtin_nan("");
         }
         if (a.x) a.x[(size_t)b * n + i] = v;
-        if (i == 0 && a.mpc && status == kSolved) a.U[b] = Uv + v;  // U += x(0)  (:105)
+        if (i == 0 && a.mpc_u && status == kSolved) a.U[b] = Uv + v;  // U += x(0)  (:105)
     }
     if (a.y) {
 #pragma unroll
@@ -468,32 +469,27 @@ void admm_lane_kernel(AdmmArgs<T> a)
     a.rho_out[b] = (double)rho;
 }
 
-// osqp_warm_start: x^ = Dinv x, x' = W^-1 x^, z = A^ x^, y^ = c Einv y  (all QPs).
-template <typename T, int NC, int MC>
-__global__ __launch_bounds__(64) void warm_start_kernel(AdmmArgs<T> a, const double *x, const double *y)
+// osqp_warm_start: x^ = Dinv x, x' = W^-1 x^, z = A^ x^, y^ = c Einv y  (all QPs).  Cold path with
+// runtime capacities (nc, mc): serves the lane kernel's and the tile kernel's state layout alike.
+template <typename T>
+__global__ __launch_bounds__(64) void warm_start_kernel(AdmmArgs<T> a, int nc, int mc, const double *x, const double *y)
 {
     const int b = blockIdx.x * 64 + threadIdx.x;
     if (b >= a.batch) return;
-    const int n = a.n, m = a.m, B = a.batch;
+    const int n = a.n, m = a.m;
     const size_t po = a.shared ? 0 : (size_t)b * a.ops_stride;
-    PlantOps<T> op = a.ops;
-    T xh[NC];
-    #pragma unroll
-    for (int k = 0; k < NC; k++) xh[k] = k < n ? (T)(x[(size_t)b * n + k] * (double)op.Dinv[po + k]) : T(0);
-    #pragma unroll
-    for (int k = 0; k < NC; k++) {
+    const PlantOps<T> op = a.ops;
+    auto xh = [&](int i) -> T { return i < n ? (T)(x[(size_t)b * n + i] * (double)op.Dinv[po + i]) : T(0); };
+    for (int k = 0; k < nc; k++) {
         T s = 0;
-        #pragma unroll
-        for (int i = 0; i < NC; i++) s = tfma(op.Winv[po + k * NC + i], xh[i], s);
-        a.xs[(size_t)b * NC + k] = s;
+        for (int i = 0; i < nc; i++) s = tfma(op.Winv[po + (size_t)k * nc + i], xh(i), s);
+        a.xs[(size_t)b * nc + k] = s;
     }
-    #pragma unroll
-    for (int j = 0; j < MC; j++) {
+    for (int j = 0; j < mc; j++) {
         T s = 0;
-        #pragma unroll
-        for (int k = 0; k < NC; k++) s = tfma(op.Ah[po + j * NC + k], xh[k], s);
-        a.zs[(size_t)b * MC + j] = s;
-        a.ys[(size_t)b * MC + j] =
+        for (int k = 0; k < nc; k++) s = tfma(op.Ah[po + (size_t)j * nc + k], xh(k), s);
+        a.zs[(size_t)b * mc + j] = s;
+        a.ys[(size_t)b * mc + j] =
             j < m ? (T)((y[(size_t)b * m + j] * (double)op.Einv[po + j]) * (double)op.cs[po]) : T(0);
     }
 }
@@ -528,52 +524,9 @@ static int launch_any(const AdmmArgs<T> &a, int nc, int mc, hipStream_t s)
 template <typename T>
 static int warm_any(const AdmmArgs<T> &a, int nc, int mc, const double *x, const double *y, hipStream_t s)
 {
-    const dim3 grid((a.batch + 63) / 64), block(64);
-#define MPCQ_TRY(NC_, MC_) \
-    if (nc == NC_ && mc == MC_) { hipLaunchKernelGGL((warm_start_kernel<T, NC_, MC_>), grid, block, 0, s, a, x, y); \
-                                  return hipGetLastError() == hipSuccess ? 0 : -2; }
-    MPCQ_CAPS(MPCQ_TRY)
-#undef MPCQ_TRY
-    return -1;
+    hipLaunchKernelGGL((warm_start_kernel<T>), dim3((a.batch + 63) / 64), dim3(64), 0, s, a, nc, mc, x, y);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 }  // namespace mpcq
 
-extern "C" int mpcq_internal_caps(int n, int m, int *nc, int *mc)
-{
-    int best = -1, bnc = 0, bmc = 0;
-#define MPCQ_PICK(NC_, MC_)                                              \
-    if (n <= NC_ && m <= MC_ && (best < 0 || NC_ * (NC_ + MC_) < best)) { \
-        best = NC_ * (NC_ + MC_);                                         \
-        bnc = NC_;                                                        \
-        bmc = MC_;                                                        \
-    }
-    MPCQ_CAPS(MPCQ_PICK)
-#undef MPCQ_PICK
-    if (best < 0) return -1;
-    *nc = bnc;
-    *mc = bmc;
-    return 0;
-}
-
-extern "C" int mpcq_internal_admm_launch_f64(const mpcq::AdmmArgs<double> *a, int nc, int mc, hipStream_t s)
-{
-    return mpcq::launch_any<double>(*a, nc, mc, s);
-}
-
-extern "C" int mpcq_internal_admm_launch_f32(const mpcq::AdmmArgs<float> *a, int nc, int mc, hipStream_t s)
-{
-    return mpcq::launch_any<float>(*a, nc, mc, s);
-}
-
-extern "C" int mpcq_internal_warm_f64(const mpcq::AdmmArgs<double> *a, int nc, int mc, const double *x,
-                                      const double *y, hipStream_t s)
-{
-    return mpcq::warm_any<double>(*a, nc, mc, x, y, s);
-}
-
-extern "C" int mpcq_internal_warm_f32(const mpcq::AdmmArgs<float> *a, int nc, int mc, const double *x,
-                                      const double *y, hipStream_t s)
-{
-    return mpcq::warm_any<float>(*a, nc, mc, x, y, s);
-}

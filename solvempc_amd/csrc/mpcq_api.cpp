@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -32,6 +33,8 @@ int fail(int code, const std::string &msg)
         if (e_ != hipSuccess) return fail(MPCQ_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
     } while (0)
 
+constexpr int kMaxPhases = 16;
+
 size_t setup_scratch_len(int n, int m)
 {
     return 7 * (size_t)n * n + (size_t)m * n + 3 * (size_t)n + 2 * (size_t)m + 64;
@@ -44,6 +47,11 @@ struct mpcq_ctx {
     int nc = 0, mc = 0;
     size_t ops_stride = 0;
     bool setup_done = false, all_ineq = true, mpc_ready = false, lower_free = false, fresh = false;
+    // tile (MFMA) path: shared plant with a compiled (KN, KM) shape
+    bool tile = false;
+    int KN = 0, KM = 0;
+    void *d_img = nullptr;
+    int *d_list = nullptr, *d_counts = nullptr, *d_itstate = nullptr;
     hipStream_t last = nullptr;
     int nx = 0;
     // setup
@@ -242,8 +250,16 @@ int mpcq_create(const mpcq_dims *d, const mpcq_settings *s, mpcq_ctx **out)
         st.check_termination < 0 || st.adaptive_rho_tolerance < 1 || st.adaptive_rho_interval < 0)
         return fail(MPCQ_ERR_ARG, "invalid settings (osqp validate_settings)");
     int nc = 0, mc = 0;
-    if (mpcq_internal_caps(d->n, std::max(d->m, 1), &nc, &mc) != 0)
+    const int KN = (d->n + 3) / 4, KM = (std::max(d->m, 1) + 3) / 4;
+    const char *force = std::getenv("MPCQ_KERNEL");  // test hook: "lane" forces the per-lane kernel
+    const bool tile = d->n_plants == 1 && mpcq_internal_tile_supported(KN, KM) &&
+                      !(force && std::strcmp(force, "lane") == 0);
+    if (tile) {
+        nc = 16 * ((KN + 3) / 4);
+        mc = 16 * ((KM + 3) / 4);
+    } else if (mpcq_internal_caps(d->n, std::max(d->m, 1), &nc, &mc) != 0) {
         return fail(MPCQ_ERR_ARG, "n/m exceed the compiled kernel capacities (n <= 32, m <= 64)");
+    }
 
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= d->device || d->device < 0)
@@ -260,6 +276,9 @@ int mpcq_create(const mpcq_dims *d, const mpcq_settings *s, mpcq_ctx **out)
     c->set = st;
     c->nc = nc;
     c->mc = mc;
+    c->tile = tile;
+    c->KN = KN;
+    c->KM = KM;
     const mpcq::OpsLayout L = mpcq::OpsLayout::make(nc, mc);
     c->ops_stride = L.total;
     const size_t P = d->n_plants, B = d->batch, n = d->n, m = d->m;
@@ -291,8 +310,16 @@ int mpcq_create(const mpcq_dims *d, const mpcq_settings *s, mpcq_ctx **out)
     A(&c->d_zs, es * B * mc);
     A(&c->d_ys, es * B * mc);
     A(&c->d_rhos, es * B);
-    A(&c->d_snx, es * B * nc);
-    A(&c->d_sny, es * B * mc);
+    if (tile) {
+        const mpcq::TileLayout TL = mpcq::TileLayout::make(KN, KM, (int)(16 / es));
+        A(&c->d_img, es * TL.total);
+        A((void **)&c->d_list, 4 * 2 * B);
+        A((void **)&c->d_counts, 4 * kMaxPhases);
+        A((void **)&c->d_itstate, 4 * B);
+    } else {
+        A(&c->d_snx, es * B * nc);
+        A(&c->d_sny, es * B * mc);
+    }
     if (!ok) {
         mpcq_destroy(c);
         return fail(MPCQ_ERR_HIP, "hipMalloc failed");
@@ -310,7 +337,8 @@ int mpcq_destroy(mpcq_ctx *c)
     void *ptrs[] = {c->d_P, c->d_q0, c->d_A, c->d_l0, c->d_u0, c->d_ops, c->d_ops32, c->d_scratch, c->d_ctype,
                     c->d_setup_status, c->d_q, c->d_u, c->d_l, c->d_x, c->d_y, c->d_rho, c->d_status, c->d_iter,
                     c->d_xs, c->d_zs, c->d_ys, c->d_rhos, c->d_snx, c->d_sny, c->d_Fx, c->d_Fu, c->d_Fr,
-                    c->d_Sbar, c->d_Ku, c->d_W0, c->d_X, c->d_U};
+                    c->d_Sbar, c->d_Ku, c->d_W0, c->d_X, c->d_U, c->d_img, c->d_list, c->d_counts,
+                    c->d_itstate};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete c;
@@ -362,6 +390,9 @@ int mpcq_setup(mpcq_ctx *c, const double *P, const double *q0, const double *A, 
     if (c->dims.dtype == MPCQ_F32 &&
         mpcq_internal_f64_to_f32(c->d_ops, c->d_ops32, Pn * c->ops_stride, s) != 0)
         return fail(MPCQ_ERR_HIP, "operator conversion failed");
+    if (c->tile && mpcq_internal_tile_images(c->d_ops, c->nc, c->mc, c->KN, c->KM, c->dims.dtype == MPCQ_F32,
+                                             c->d_img, s) != 0)
+        return fail(MPCQ_ERR_HIP, "tile image kernel failed");
     const int per = Pn > 1;
     if (mpcq_internal_broadcast(c->d_q0, c->d_q, (int)n, (int)B, per, s) ||
         mpcq_internal_broadcast(c->d_u0, c->d_u, (int)m, (int)B, per, s) ||
@@ -441,26 +472,76 @@ int mpcq_warm_start(mpcq_ctx *c, const double *x, const double *y)
     return MPCQ_OK;
 }
 
+}  // extern "C"
+
+// Phase boundaries of the tile path (multiples of check_termination, then max_iter): QPs still
+// running at a boundary are re-packed densely into the waves of the next launch.
+static int phase_stops(const mpcq_settings &st, int *stops)
+{
+    const int ct = st.check_termination;
+    int np = 0;
+    if (ct > 0) {
+        static const int mult[] = {3, 4, 5, 6, 8, 12, 20, 40, 80, 160};
+        for (int k : mult) {
+            const long it = (long)k * ct;
+            if (it >= st.max_iter || np >= kMaxPhases - 1) break;
+            stops[np++] = (int)it;
+        }
+    }
+    stops[np++] = st.max_iter;
+    return np;
+}
+
+template <typename T>
+static int launch_args(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s)
+{
+    if (!c->tile) {
+        const int rc = std::is_same<T, float>::value
+                           ? mpcq_internal_admm_launch_f32((const mpcq::AdmmArgs<float> *)&a, c->nc, c->mc, s)
+                           : mpcq_internal_admm_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->nc, c->mc, s);
+        return rc;
+    }
+    int stops[kMaxPhases];
+    const int np = phase_stops(c->set, stops);
+    if (hipMemsetAsync(c->d_counts, 0, 4 * kMaxPhases, s) != hipSuccess) return -2;
+    const int B = c->dims.batch;
+    const int mpc = a.mpc;
+    for (int p = 0; p < np; p++) {
+        a.img = (const T *)c->d_img;
+        a.list_in = p ? c->d_list + (size_t)(p % 2) * B : nullptr;
+        a.count_in = p ? c->d_counts + (p - 1) : nullptr;
+        a.list_out = c->d_list + (size_t)((p + 1) % 2) * B;
+        a.count_out = c->d_counts + p;
+        a.it_state = c->d_itstate;
+        a.stop_iter = stops[p];
+        a.resume = p > 0;
+        a.mpc = p == 0 ? mpc : 0;  // later phases read q, u from the buffers phase 0 filled
+        const int rc = std::is_same<T, float>::value
+                           ? mpcq_internal_tile_launch_f32((const mpcq::AdmmArgs<float> *)&a, c->KN, c->KM, s)
+                           : mpcq_internal_tile_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->KN, c->KM, s);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+template <typename T>
+static int launch_typed(mpcq_ctx *c, hipStream_t s, bool mpc, const double *X, double *U, double xref)
+{
+    auto a = make_args<T>(c);
+    if (mpc) {
+        a.mpc = 1; a.mpc_u = 1; a.nx = c->nx; a.X = X; a.U = U; a.xref = xref;
+        a.Fx = c->d_Fx; a.Fu = c->d_Fu; a.Fr = c->d_Fr; a.Sbar = c->d_Sbar; a.Ku = c->d_Ku; a.W0 = c->d_W0;
+        a.q_out = c->d_q; a.u_out = c->d_u;
+    }
+    return launch_args<T>(c, a, s);
+}
+
+extern "C" {
+
 static int launch_solve(mpcq_ctx *c, hipStream_t s, bool mpc, const double *X, double *U, double xref)
 {
-    int rc;
-    if (c->dims.dtype == MPCQ_F32) {
-        auto a = make_args<float>(c);
-        if (mpc) {
-            a.mpc = 1; a.nx = c->nx; a.X = X; a.U = U; a.xref = xref;
-            a.Fx = c->d_Fx; a.Fu = c->d_Fu; a.Fr = c->d_Fr; a.Sbar = c->d_Sbar; a.Ku = c->d_Ku; a.W0 = c->d_W0;
-            a.q_out = c->d_q; a.u_out = c->d_u;
-        }
-        rc = mpcq_internal_admm_launch_f32(&a, c->nc, c->mc, s);
-    } else {
-        auto a = make_args<double>(c);
-        if (mpc) {
-            a.mpc = 1; a.nx = c->nx; a.X = X; a.U = U; a.xref = xref;
-            a.Fx = c->d_Fx; a.Fu = c->d_Fu; a.Fr = c->d_Fr; a.Sbar = c->d_Sbar; a.Ku = c->d_Ku; a.W0 = c->d_W0;
-            a.q_out = c->d_q; a.u_out = c->d_u;
-        }
-        rc = mpcq_internal_admm_launch_f64(&a, c->nc, c->mc, s);
-    }
+    const int rc = c->dims.dtype == MPCQ_F32 ? launch_typed<float>(c, s, mpc, X, U, xref)
+                                             : launch_typed<double>(c, s, mpc, X, U, xref);
     if (rc) return fail(MPCQ_ERR_HIP, std::string("ADMM kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
     c->last = s;
     c->fresh = false;

@@ -136,7 +136,49 @@ struct AdmmArgs {
     const double *X, *Fx, *Fu, *Fr, *Sbar, *Ku, *W0;
     double *U, *q_out, *u_out;
     double xref;
+    int mpc_u;                  // U += x[0] at termination (the front end may have run in an earlier phase)
+    // tile kernel (shared plant): MFMA operand images and the phase machinery (mpcq_tile.h)
+    const T *img;               // TileLayout images of the plant
+    const int *list_in;         // active QP indices of this phase (null: identity 0..batch-1)
+    const int *count_in;        // device count of list_in (null: batch)
+    int *list_out, *count_out;  // QPs still running at stop_iter (appended)
+    int *it_state;              // [batch] iterations done so far in this solve
+    int stop_iter;              // phase boundary (multiple of check_termination, or max_iter)
+    int resume;                 // 1: phase >= 2 (state, rho and iteration count come from the buffers)
 };
+
+// MFMA operand images of one shared plant for the tile kernel (mpcq_tile.h).  A vector of length
+// 4*KS is held in "D-layout": lane l = 16 g + c (column c = QP, group g) keeps element 4 s + g of
+// its QP in register s.  Image (tile t, k-step s, lane l) = M[16 t + arow(l & 15)][4 s + (l >> 4)],
+// stored [t][s / VEC][lane][s % VEC] so one lane reads VEC consecutive k-steps with one 16-B load.
+struct TileLayout {
+    int KN, KM, NT, MT, VEC, KNP, KMP;
+    size_t S, Bt, B, PW, AhT, W, Wt, total;
+    __host__ __device__ static constexpr TileLayout make(int KN, int KM, int VEC)
+    {
+        TileLayout L{};
+        L.KN = KN; L.KM = KM; L.VEC = VEC;
+        L.NT = (KN + 3) / 4; L.MT = (KM + 3) / 4;
+        L.KNP = (KN + VEC - 1) / VEC * VEC; L.KMP = (KM + VEC - 1) / VEC * VEC;
+        size_t o = 0;
+        L.S = o;   o += (size_t)L.NT * L.KNP * 64;   // sigma W'W       (n x n)
+        L.Bt = o;  o += (size_t)L.NT * L.KMP * 64;   // B' = (A^ W)'    (n x m)
+        L.B = o;   o += (size_t)L.MT * L.KNP * 64;   // B = A^ W        (m x n)
+        L.PW = o;  o += (size_t)L.NT * L.KNP * 64;   // P^ W            (n x n)
+        L.AhT = o; o += (size_t)L.NT * L.KMP * 64;   // A^'             (n x m)
+        L.W = o;   o += (size_t)L.NT * L.KNP * 64;   // W               (n x n)
+        L.Wt = o;  o += (size_t)L.NT * L.KNP * 64;   // W'              (n x n)
+        L.total = o;
+        return L;
+    }
+    __host__ __device__ static constexpr size_t at(int KSP, int VEC, int t, int s, int lane)
+    {
+        return ((size_t)(t * (KSP / VEC) + s / VEC) * 64 + lane) * VEC + (s % VEC);
+    }
+};
+// A-operand row i of an output tile holds logical row arow(i): the f32 16x16x4 accumulator keeps
+// rows 4g + r of a tile in lane group g, register r; the f64 one keeps rows g + 4r.
+__host__ __device__ constexpr int tile_arow(int is_f32, int i) { return is_f32 ? 4 * (i & 3) + (i >> 2) : i; }
 
 }  // namespace mpcq
 
@@ -164,4 +206,11 @@ int mpcq_internal_warm_f64(const mpcq::AdmmArgs<double> *a, int nc, int mc, cons
                            hipStream_t s);
 int mpcq_internal_warm_f32(const mpcq::AdmmArgs<float> *a, int nc, int mc, const double *x, const double *y,
                            hipStream_t s);
+// Tile (MFMA) path for a shared plant: 0 = launched, -1 = (KN, KM) not compiled, -2 = HIP error.
+int mpcq_internal_tile_supported(int KN, int KM);
+int mpcq_internal_tile_launch_f64(const mpcq::AdmmArgs<double> *a, int KN, int KM, hipStream_t s);
+int mpcq_internal_tile_launch_f32(const mpcq::AdmmArgs<float> *a, int KN, int KM, hipStream_t s);
+// Build the TileLayout images (type T = f32 if is_f32) of plant 0 from its fp64 operator block.
+int mpcq_internal_tile_images(const double *ops, int nc, int mc, int KN, int KM, int is_f32, void *img,
+                              hipStream_t s);
 }

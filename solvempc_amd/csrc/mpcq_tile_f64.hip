@@ -1,0 +1,7 @@
+// solvempc_amd/csrc/mpcq_tile_f64.hip — fp64 instantiations of the tile (MFMA) ADMM kernel.
+#include "mpcq_tile.h"
+
+extern "C" int mpcq_internal_tile_launch_f64(const mpcq::AdmmArgs<double> *a, int KN, int KM, hipStream_t s)
+{
+    return mpcq::tile_launch_any<double>(*a, KN, KM, s);
+}
