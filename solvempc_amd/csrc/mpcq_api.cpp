@@ -480,7 +480,8 @@ static int phase_stops(const mpcq_settings &st, int *stops)
 {
     const int ct = st.check_termination;
     int np = 0;
-    if (ct > 0) {
+    const char *e = std::getenv("MPCQ_PHASES");  // test/benchmark hook: "0" = one launch per solve
+    if (ct > 0 && !(e && e[0] == '0')) {
         static const int mult[] = {3, 4, 5, 6, 8, 12, 20, 40, 80, 160};
         for (int k : mult) {
             const long it = (long)k * ct;

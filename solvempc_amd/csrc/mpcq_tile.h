@@ -23,6 +23,7 @@
 #pragma once
 #include "mpcq_internal.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace mpcq {
@@ -49,28 +50,69 @@ template <> __device__ __forceinline__ double tt_fma(double a, double b, double 
 template <typename T> __device__ __forceinline__ T tt_abs(T a) { return a < T(0) ? -a : a; }
 template <typename T> __device__ __forceinline__ T tt_max(T a, T b) { return a > b ? a : b; }
 template <typename T> __device__ __forceinline__ T tt_min(T a, T b) { return a < b ? a : b; }
+// max(m, |x|) for the infinity norms (one v_max with an |.| source modifier; equals OSQP's
+// c_max(m, c_absval(x)) for every non-NaN x).
+template <typename T> __device__ __forceinline__ T nrm(T m, T x) { return __builtin_fmax(m, __builtin_fabs(x)); }
 
-// Reductions over the 4 lanes (groups) of one QP column.  Identical result on all 4 lanes.
+// Reductions over the 4 lanes (groups) of one QP column (lanes c, c+16, c+32, c+48) with the gfx950
+// lane-swap instructions (v_permlane16_swap / v_permlane32_swap: VALU, no LDS round trip).  After a
+// swap of v with itself, {r[0], r[1]} = {own value, partner's value} in some order, so a symmetric
+// op of the pair gives the same, bit-identical result on all lanes of the column.
+template <typename F>
+__device__ __forceinline__ unsigned swap_combine(unsigned v, F op)
+{
+    auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    v = op(r[0], r[1]);
+    auto t = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return op(t[0], t[1]);
+}
+template <typename T, typename F> __device__ __forceinline__ T col_reduce(T v, F op);
+template <typename F> __device__ __forceinline__ float col_reduce(float v, F op)
+{
+    return __uint_as_float(swap_combine(__float_as_uint(v), [&](unsigned a, unsigned b) {
+        return __float_as_uint(op(__uint_as_float(a), __uint_as_float(b)));
+    }));
+}
+template <typename F> __device__ __forceinline__ double col_reduce(double v, F op)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+    auto r = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    auto mk = [](unsigned l, unsigned hh) { return __longlong_as_double((long long)(((unsigned long long)hh << 32) | l)); };
+    double w = op(mk(r[0], h[0]), mk(r[1], h[1]));
+    const unsigned long long u2 = (unsigned long long)__double_as_longlong(w);
+    lo = (unsigned)u2;
+    hi = (unsigned)(u2 >> 32);
+    auto r2 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    auto h2 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    return op(mk(r2[0], h2[0]), mk(r2[1], h2[1]));
+}
 template <typename T> __device__ __forceinline__ T col_max(T v)
 {
-    v = tt_max(v, (T)__shfl_xor(v, 16));
-    return tt_max(v, (T)__shfl_xor(v, 32));
+    return col_reduce(v, [](T a, T b) { return __builtin_fmax(a, b); });
 }
 template <typename T> __device__ __forceinline__ T col_sum(T v)
 {
-    v = v + (T)__shfl_xor(v, 16);
-    return v + (T)__shfl_xor(v, 32);
+    return col_reduce(v, [](T a, T b) { return a + b; });
 }
 __device__ __forceinline__ int col_or(int v)
 {
-    v |= __shfl_xor(v, 16);
-    return v | __shfl_xor(v, 32);
+    return (int)swap_combine((unsigned)v, [](unsigned a, unsigned b) { return a | b; });
 }
 __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0ull; }
 __device__ __forceinline__ bool wave_all(bool p) { return __ballot(!p) == 0ull; }
 
 // Hide a pointer's provenance from LICM: the images are re-read from LDS in every phase of every
 // iteration instead of being hoisted into (and spilling) registers.
+// An opaque copy of a per-lane index: addresses derived from it are recomputed where they are used
+// (cold paths) instead of being kept live, as 64-bit VGPR pairs, across the hot loop.
+__device__ __forceinline__ int opaque(int v)
+{
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
 template <typename P> __device__ __forceinline__ P fresh_ptr(P p)
 {
     int zero;
@@ -78,34 +120,42 @@ template <typename P> __device__ __forceinline__ P fresh_ptr(P p)
     return p + zero;
 }
 
-// y[0 .. 4 NTO) = init + M x over KS k-steps, M an LDS image with KSP padded k-steps.
+// y[0 .. 4 NTO) = init + M x over KS k-steps, M an LDS image with KSP padded k-steps.  All the
+// operands of the product are read first (16-B ds_reads, one counted wait), then the NTO independent
+// accumulator chains are interleaved k-step by k-step so that no MFMA waits on its predecessor's
+// result (16x16x4: 32-cycle issue, 40-cycle dependent latency).
 template <typename T, int NTO, int KS, int KSP, int XN>
 __device__ __forceinline__ void tile_mv(const T *__restrict__ im, const T (&x)[XN], T (&y)[4 * NTO], int lane,
                                         const T *init)
 {
     using A = typename Mf<T>::acc;
     constexpr int VEC = 16 / sizeof(T);
+    constexpr int NG = (KS + VEC - 1) / VEC;
     typedef T vec __attribute__((ext_vector_type(VEC)));
     im = fresh_ptr(im);
+    vec opnd[NTO][NG];
 #pragma unroll
-    for (int t = 0; t < NTO; t++) {
-        A acc;
+    for (int t = 0; t < NTO; t++)
 #pragma unroll
-        for (int r = 0; r < 4; r++) acc[r] = init ? init[4 * t + r] : T(0);
+        for (int q = 0; q < NG; q++) opnd[t][q] = *(const vec *)(im + TileLayout::at(KSP, VEC, t, q * VEC, lane));
+    A acc[NTO];
 #pragma unroll
-        for (int s0 = 0; s0 < KS; s0 += VEC) {
-            const vec v = *(const vec *)(im + TileLayout::at(KSP, VEC, t, s0, lane));
+    for (int t = 0; t < NTO; t++)
 #pragma unroll
-            for (int e = 0; e < VEC; e++)
-                if (s0 + e < KS) acc = Mf<T>::mma(v[e], x[s0 + e], acc);
-        }
+        for (int r = 0; r < 4; r++) acc[t][r] = init ? init[4 * t + r] : T(0);
 #pragma unroll
-        for (int r = 0; r < 4; r++) y[4 * t + r] = acc[r];
-    }
+    for (int s = 0; s < KS; s++)
+#pragma unroll
+        for (int t = 0; t < NTO; t++) acc[t] = Mf<T>::mma(opnd[t][s / VEC][s % VEC], x[s], acc[t]);
+#pragma unroll
+    for (int t = 0; t < NTO; t++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) y[4 * t + r] = acc[t][r];
 }
 
-template <typename T, int KN, int KM, bool ALL_INEQ, bool LFREE>
-__global__ __launch_bounds__(256, (sizeof(T) == 4 && ALL_INEQ && LFREE) ? 4 : 2) void admm_tile_kernel(AdmmArgs<T> a)
+// OCC: waves per SIMD the register allocation is held to (256-thread workgroups).
+template <typename T, int KN, int KM, bool ALL_INEQ, bool LFREE, int OCC>
+__global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
 {
     constexpr int VEC = 16 / sizeof(T);
     constexpr TileLayout L = TileLayout::make(KN, KM, VEC);
@@ -113,9 +163,22 @@ __global__ __launch_bounds__(256, (sizeof(T) == 4 && ALL_INEQ && LFREE) ? 4 : 2)
     constexpr int NS = 4 * NT, MS = 4 * MT;  // registers per n- / m-vector
     constexpr int is32 = sizeof(T) == 4;
     (void)is32;
+    constexpr int NCP = 16 * NT, MCP = 16 * MT;  // padded row counts (== ctx nc, mc)
     __shared__ __attribute__((aligned(16))) T img[L.total];
+    __shared__ T rowv[3 * NCP + 2 * MCP];        // lam, D, Dinv | E, Einv of the plant
+    T *const s_lam = rowv, *const s_D = rowv + NCP, *const s_Dinv = rowv + 2 * NCP;
+    T *const s_E = rowv + 3 * NCP, *const s_Einv = rowv + 3 * NCP + MCP;
     const int count = a.count_in ? *a.count_in : a.batch;
     if (blockIdx.x * 64 >= count) return;  // whole workgroup idle in this phase (uniform)
+    for (int i = threadIdx.x; i < NCP; i += 256) {
+        s_lam[i] = a.ops.lam[i];
+        s_D[i] = a.ops.D[i];
+        s_Dinv[i] = a.ops.Dinv[i];
+    }
+    for (int i = threadIdx.x; i < MCP; i += 256) {
+        s_E[i] = a.ops.E[i];
+        s_Einv[i] = a.ops.Einv[i];
+    }
 
     // ---- plant images -> LDS (16 B per thread per step)
     {
@@ -130,7 +193,8 @@ __global__ __launch_bounds__(256, (sizeof(T) == 4 && ALL_INEQ && LFREE) ? 4 : 2)
     const int wave_slot = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
     if (wave_slot >= count) return;
     const bool valid = wave_slot + c < count;
-    const int b = valid ? (a.list_in ? a.list_in[wave_slot + c] : wave_slot + c) : 0;
+    const int b_ = valid ? (a.list_in ? a.list_in[wave_slot + c] : wave_slot + c) : 0;
+    int b = b_;
     const int n = a.n, m = a.m;
     const int ncs = 4 * NT * 4, mcs = 4 * MT * 4;  // state row strides (ctx nc = 16 NT, mc = 16 MT)
     const PlantOps<T> op = a.ops;                  // shared plant: block 0
@@ -148,7 +212,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 4 && ALL_INEQ && LFREE) ? 4 : 2)
             if (t < a.nx) Xv[t] = a.X[(size_t)b * a.nx + t];
     }
     if (a.mpc_u) Uv = a.U[b];
-    T qh[NS];  // q^, only until g = W' q^ is formed (checks re-read q)
+    T qh[NS];  // q^ = c D q (osqp_update_lin_cost), kept for the dual residual
 #pragma unroll
     for (int s = 0; s < NS; s++) {
         const int v = 4 * s + g;
@@ -210,7 +274,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 4 && ALL_INEQ && LFREE) ? 4 : 2)
     T gv[NS];
     tile_mv<T, NT, KN, KNP>(img + L.Wt, qh, gv, lane, (const T *)nullptr);
 #pragma unroll
-    for (int s = 0; s < NS; s++) gv[s] = -gv[s];  // xi starts from -g
+    for (int s = 0; s < NS; s++) gv[s] = s < KN ? -gv[s] : T(0);  // xi starts from -g (padding rows 0)
 
     // ---- state: x' (W-basis), z, y; rho persists across solves (OSQP)
     T xs[NS], z[MS], y[MS];
@@ -234,7 +298,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 4 && ALL_INEQ && LFREE) ? 4 : 2)
     T rinv = T(1) / rho;
     T dk[NS];
     auto set_dk = [&]() {
-        const T *lam = fresh_ptr(op.lam);
+        const T *lam = fresh_ptr((const T *)s_lam);
 #pragma unroll
         for (int s = 0; s < NS; s++) dk[s] = T(1) / (T(1) + rho * lam[4 * s + g]);  // lam padded with 0
     };
@@ -246,6 +310,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 4 && ALL_INEQ && LFREE) ? 4 : 2)
 
     // ---- write one QP's results (OSQP store_solution / update_info; warm-start state)
     auto finalize = [&](bool mine) {
+        const int b = opaque(b_);
         // x = D W x'  (all lanes run the MFMA; `mine` lanes store)
         T xh[NS];
         tile_mv<T, NT, KN, KNP>(img + L.W, xs, xh, lane, (const T *)nullptr);
@@ -256,16 +321,16 @@ __global__ __launch_bounds__(256, (sizeof(T) == 4 && ALL_INEQ && LFREE) ? 4 : 2)
         for (int s = 0; s < NS; s++) {
             const int v = 4 * s + g;
             if (s < KN && v < n) {
-                const double xv = has_sol ? (double)xh[s] * (double)op.D[v] : __builtin_nan("");
+                const double xv = has_sol ? (double)xh[s] * (double)s_D[v] : __builtin_nan("");
                 if (a.x) a.x[(size_t)b * n + v] = xv;
-                if (v == 0 && a.mpc_u && status == kSolved) a.U[b] = Uv + xv;  // U += x(0)  (:105)
+                if (v == 0 && a.mpc_u && status == kSolved) a.U[b] = a.U[b] + xv;  // U += x(0)  (:105)
             }
         }
 #pragma unroll
         for (int s = 0; s < MS; s++) {
             const int v = 4 * s + g;
             if (s < KM && v < m && a.y)
-                a.y[(size_t)b * m + v] = has_sol ? ((double)y[s] * (double)op.E[v]) * cinv64 : __builtin_nan("");
+                a.y[(size_t)b * m + v] = has_sol ? ((double)y[s] * (double)s_E[v]) * cinv64 : __builtin_nan("");
         }
         const bool keep = has_sol || status == kInvalidBounds || status == kTypeChanged;
 #pragma unroll
@@ -292,11 +357,16 @@ __global__ __launch_bounds__(256, (sizeof(T) == 4 && ALL_INEQ && LFREE) ? 4 : 2)
     }
 
     const int ct = st.check_termination;
+    const int ai = (st.adaptive_rho && a.adaptive_interval) ? a.adaptive_interval : 0;
     const int stop = a.stop_iter;
+    int next_check = ct ? (it / ct + 1) * ct : -1;  // uniform; no integer division in the loop
+    int next_adapt = ai ? (it / ai + 1) * ai : -1;
     while (!wave_all(done)) {
         it++;
-        const bool at_check = ct && (it % ct == 0);
-        const bool at_adapt = st.adaptive_rho && a.adaptive_interval && (it % a.adaptive_interval == 0);
+        const bool at_check = it == next_check;
+        const bool at_adapt = it == next_adapt;
+        if (at_check) next_check += ct;
+        if (at_adapt) next_adapt += ai;
         const bool last = it == st.max_iter;
         const bool info = at_check || at_adapt || last || it == stop;
 
@@ -318,7 +388,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 4 && ALL_INEQ && LFREE) ? 4 : 2)
             tile_mv<T, NT, KM, KMP>(img + L.Bt, wz, xi, lane, xi);  //    + B' w
             // eta = xi / (1 + rho lambda) ; x' = alpha eta + (1 - alpha) x'
 #pragma unroll
-            for (int s = 0; s < NS; s++) {
+            for (int s = 0; s < KN; s++) {  // registers s >= KN are padding rows: x' stays 0 there
                 xi[s] = xi[s] * dk[s];
                 const T xn = tt_fma(alpha, xi[s], oma * xs[s]);
                 if (DELTA) dx[s] = xn - xs[s];
@@ -335,8 +405,8 @@ __global__ __launch_bounds__(256, (sizeof(T) == 4 && ALL_INEQ && LFREE) ? 4 : 2)
                 }
                 const T v = tt_fma(alpha, wz[s], oma * z[s]);
                 T zn = tt_fma(rij, y[s], v);
-                if (!LFREE) zn = tt_max(zn, lh[s]);
-                zn = tt_min(zn, uh[s]);
+                if (!LFREE) zn = __builtin_fmax(zn, lh[s]);  // == OSQP's c_max/c_min, NaN included
+                zn = __builtin_fmin(zn, uh[s]);
                 const T d = rj * (v - zn);
                 if (DELTA) dy[s] = d;
                 y[s] = y[s] + d;
@@ -356,17 +426,17 @@ __global__ __launch_bounds__(256, (sizeof(T) == 4 && ALL_INEQ && LFREE) ? 4 : 2)
         {
             T ax[MS];
             tile_mv<T, MT, KN, KNP>(img + L.B, xs, ax, lane, (const T *)nullptr);
-            const T *Einv = fresh_ptr(op.Einv);
+            const T *Einv = fresh_ptr((const T *)s_Einv);
 #pragma unroll
             for (int s = 0; s < KM; s++) {
                 const T r = ax[s] - z[s];
                 const T ei = Einv[4 * s + g];
-                ax_z = tt_max(ax_z, tt_abs(r));
-                ax_zs = tt_max(ax_zs, tt_abs(ei * r));
-                zn_r = tt_max(zn_r, tt_abs(z[s]));
-                zn_s = tt_max(zn_s, tt_abs(ei * z[s]));
-                axn_r = tt_max(axn_r, tt_abs(ax[s]));
-                axn_s = tt_max(axn_s, tt_abs(ei * ax[s]));
+                ax_z = nrm(ax_z, r);
+                ax_zs = nrm(ax_zs, ei * r);
+                zn_r = nrm(zn_r, z[s]);
+                zn_s = nrm(zn_s, ei * z[s]);
+                axn_r = nrm(axn_r, ax[s]);
+                axn_s = nrm(axn_s, ei * ax[s]);
             }
         }
         T dr_r = 0, dr_s = 0, qn_r = 0, qn_s = 0, atyn_r = 0, atyn_s = 0, pxn_r = 0, pxn_s = 0;
@@ -374,23 +444,20 @@ __global__ __launch_bounds__(256, (sizeof(T) == 4 && ALL_INEQ && LFREE) ? 4 : 2)
             T px[NS], aty[NS];
             tile_mv<T, NT, KN, KNP>(img + L.PW, xs, px, lane, (const T *)nullptr);
             tile_mv<T, NT, KM, KMP>(img + L.AhT, y, aty, lane, (const T *)nullptr);
-            const T *Dinv = fresh_ptr(op.Dinv);
-            const T *Dq = fresh_ptr(op.D);
-            const double *qsrc = a.mpc ? a.q_out : a.q;
+            const T *Dinv = fresh_ptr((const T *)s_Dinv);
 #pragma unroll
             for (int s = 0; s < KN; s++) {
-                const int v = 4 * s + g;
-                const T qhs = v < n ? (T)((qsrc[(size_t)b * n + v] * (double)Dq[v]) * c64) : T(0);
+                const T qhs = qh[s];
                 const T r = (qhs + px[s]) + aty[s];
                 const T di = Dinv[4 * s + g];
-                dr_r = tt_max(dr_r, tt_abs(r));
-                dr_s = tt_max(dr_s, tt_abs(di * r));
-                qn_r = tt_max(qn_r, tt_abs(qhs));
-                qn_s = tt_max(qn_s, tt_abs(di * qhs));
-                atyn_r = tt_max(atyn_r, tt_abs(aty[s]));
-                atyn_s = tt_max(atyn_s, tt_abs(di * aty[s]));
-                pxn_r = tt_max(pxn_r, tt_abs(px[s]));
-                pxn_s = tt_max(pxn_s, tt_abs(di * px[s]));
+                dr_r = nrm(dr_r, r);
+                dr_s = nrm(dr_s, di * r);
+                qn_r = nrm(qn_r, qhs);
+                qn_s = nrm(qn_s, di * qhs);
+                atyn_r = nrm(atyn_r, aty[s]);
+                atyn_s = nrm(atyn_s, di * aty[s]);
+                pxn_r = nrm(pxn_r, px[s]);
+                pxn_s = nrm(pxn_s, di * px[s]);
             }
         }
         ax_z = col_max(ax_z); ax_zs = col_max(ax_zs); zn_s = col_max(zn_s); zn_r = col_max(zn_r);
@@ -405,7 +472,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 4 && ALL_INEQ && LFREE) ? 4 : 2)
         auto primal_infeasible = [&](T eps, bool need) -> bool {
             T d[MS];
             T ndy = 0, lhs = 0;
-            const T *E = fresh_ptr(op.E);
+            const T *E = fresh_ptr((const T *)s_E);
 #pragma unroll
             for (int s = 0; s < MS; s++) {
                 if (s >= KM) { d[s] = T(0); continue; }
@@ -415,7 +482,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 4 && ALL_INEQ && LFREE) ? 4 : 2)
                 if (uinf) dd = linf ? T(0) : tt_min(dd, T(0));
                 else if (linf) dd = tt_max(dd, T(0));
                 d[s] = dd;
-                ndy = tt_max(ndy, tt_abs(scaled_term ? dd : E[4 * s + g] * dd));
+                ndy = nrm(ndy, scaled_term ? dd : E[4 * s + g] * dd);
                 if (up < T(kInfty * kMinScaling)) lhs += up * tt_max(dd, T(0));
                 if (lo > T(-kInfty * kMinScaling)) lhs += lo * tt_min(dd, T(0));
             }
@@ -425,10 +492,10 @@ __global__ __launch_bounds__(256, (sizeof(T) == 4 && ALL_INEQ && LFREE) ? 4 : 2)
             if (!wave_any(cand)) return false;
             T atd[NS];
             tile_mv<T, NT, KM, KMP>(img + L.AhT, d, atd, lane, (const T *)nullptr);
-            const T *Dinv = fresh_ptr(op.Dinv);
+            const T *Dinv = fresh_ptr((const T *)s_Dinv);
             T nat = 0;
 #pragma unroll
-            for (int s = 0; s < KN; s++) nat = tt_max(nat, tt_abs(scaled_term ? atd[s] : Dinv[4 * s + g] * atd[s]));
+            for (int s = 0; s < KN; s++) nat = nrm(nat, scaled_term ? atd[s] : Dinv[4 * s + g] * atd[s]);
             nat = col_max(nat);
             return cand && nat < eps * ndy;
         };
@@ -442,25 +509,25 @@ __global__ __launch_bounds__(256, (sizeof(T) == 4 && ALL_INEQ && LFREE) ? 4 : 2)
             if (!wave_any(cand)) return false;
             T t1[NS];
             tile_mv<T, NT, KN, KNP>(img + L.W, dx, t1, lane, (const T *)nullptr);
-            const T *D = fresh_ptr(op.D);
+            const T *D = fresh_ptr((const T *)s_D);
             T ndx = 0;
 #pragma unroll
-            for (int s = 0; s < KN; s++) ndx = tt_max(ndx, tt_abs(scaled_term ? t1[s] : D[4 * s + g] * t1[s]));
+            for (int s = 0; s < KN; s++) ndx = nrm(ndx, scaled_term ? t1[s] : D[4 * s + g] * t1[s]);
             ndx = col_max(ndx);
             const T cs = scaled_term ? T(1) : op.cs[0];
             cand = cand && ndx > T(kDivisionTol) && qdx < -cs * eps * ndx;
             if (!wave_any(cand)) return false;
             tile_mv<T, NT, KN, KNP>(img + L.PW, dx, t1, lane, (const T *)nullptr);
-            const T *Dinv = fresh_ptr(op.Dinv);
+            const T *Dinv = fresh_ptr((const T *)s_Dinv);
             T npdx = 0;
 #pragma unroll
-            for (int s = 0; s < KN; s++) npdx = tt_max(npdx, tt_abs(scaled_term ? t1[s] : Dinv[4 * s + g] * t1[s]));
+            for (int s = 0; s < KN; s++) npdx = nrm(npdx, scaled_term ? t1[s] : Dinv[4 * s + g] * t1[s]);
             npdx = col_max(npdx);
             cand = cand && npdx < cs * eps * ndx;
             if (!wave_any(cand)) return false;
             T adx[MS];
             tile_mv<T, MT, KN, KNP>(img + L.B, dx, adx, lane, (const T *)nullptr);
-            const T *Einv = fresh_ptr(op.Einv);
+            const T *Einv = fresh_ptr((const T *)s_Einv);
             int viol = 0;
 #pragma unroll
             for (int s = 0; s < KM; s++) {
@@ -526,6 +593,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 4 && ALL_INEQ && LFREE) ? 4 : 2)
         if (it == stop && !wave_all(done)) {
             // phase boundary: save the running QPs and queue them for the next launch
             const bool run = !done;
+            const int b = opaque(b_);
             if (run) {
 #pragma unroll
                 for (int s = 0; s < NS; s++)
@@ -551,14 +619,22 @@ __global__ __launch_bounds__(256, (sizeof(T) == 4 && ALL_INEQ && LFREE) ? 4 : 2)
     }
 }
 
+// occ: 0 = default for the shape/type, else a requested register budget (3 or 4 waves/SIMD) for
+// the f32 fast variant (benchmark A/B hook).
 template <typename T, int KN, int KM>
-int tile_launch(const AdmmArgs<T> &a, hipStream_t s)
+int tile_launch(const AdmmArgs<T> &a, int occ, hipStream_t s)
 {
     const dim3 grid((a.batch + 63) / 64), block(256);
-    if (a.all_ineq && a.lower_free)
-        hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true>), grid, block, 0, s, a);
-    else
-        hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, false, false>), grid, block, 0, s, a);
+    if (a.all_ineq && a.lower_free) {
+        if constexpr (sizeof(T) == 8)
+            hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 2>), grid, block, 0, s, a);
+        else if (occ == 4)
+            hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 4>), grid, block, 0, s, a);
+        else  // default: 3 waves/SIMD — the whole iteration fits in registers (no spills)
+            hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 3>), grid, block, 0, s, a);
+    } else {
+        hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, false, false, 2>), grid, block, 0, s, a);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -569,7 +645,9 @@ int tile_launch(const AdmmArgs<T> &a, hipStream_t s)
 template <typename T>
 int tile_launch_any(const AdmmArgs<T> &a, int KN, int KM, hipStream_t s)
 {
-#define MPCQ_TRY(KN_, KM_) if (KN == KN_ && KM == KM_) return tile_launch<T, KN_, KM_>(a, s);
+    const char *e = getenv("MPCQ_TILE_OCC");
+    const int occ = e ? atoi(e) : 0;
+#define MPCQ_TRY(KN_, KM_) if (KN == KN_ && KM == KM_) return tile_launch<T, KN_, KM_>(a, occ, s);
     MPCQ_TILE_SHAPES(MPCQ_TRY)
 #undef MPCQ_TRY
     return -1;
