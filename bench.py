@@ -23,7 +23,9 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3}  # MI355X vector (VALU) peaks, MI355X_MICROARCH.md / spec
+# MI355X dense matrix-core peaks (MI355X_MICROARCH.md: f32-input MFMA 157.3 TF = the f32 vector
+# peak; f64 78.6 TF).  The tile kernel's three ADMM products run on the matrix pipe.
+PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3}
 
 
 def parse():
@@ -33,7 +35,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--batch", type=int, default=65536, help="QPs per GPU")
     p.add_argument("--horizon", type=int, default=20)
-    p.add_argument("--dtype", choices=("f64", "f32"), default="f64")
+    p.add_argument("--dtype", choices=("f64", "f32"), default="f32", help="ADMM iterate type (BASELINE cfg 2: fp32)")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=0)
@@ -61,11 +63,23 @@ def cpu_baseline(ops, N, X, U, budget_s, threads):
                       f"OpenMP {nthr} threads, {dt:.2f} s"}
 
 
+def traffic_per_solve(dtype, batch, N):
+    """HBM bytes of one solve from the committed PMC pass (tools/pmc.sh -> profiles/), or None."""
+    f = ROOT / "profiles" / f"pmc_traffic_{dtype}.json"
+    try:
+        d = json.loads(f.read_text())
+    except (OSError, ValueError):
+        return None
+    if d.get("batch") != batch or d.get("horizon") != N:
+        return None
+    return d.get("bytes_per_solve")
+
+
 def main():
     a = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", str(a.gpus)))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from solvempc_amd import dist as mdist
+
+    rank, world, local = mdist.world_from_env(a.gpus)
     import torch
 
     dist = None
@@ -88,7 +102,7 @@ def main():
                            "K": plant["K"][None], "Q": [plant["Q"]], "R": [plant["R"]], "RD": [plant["RD"]]},
                           N, device=local)
     ops = {k: v[0] for k, v in ops.items()}
-    start, count = rank * B, B  # weak scaling: every rank owns B QPs of the global stream
+    start, count = mdist.weak_block(B, rank)  # weak scaling: every rank owns B QPs of the global stream
     X, U = workload.mpc_states(a.seed, start, count)
     l = np.full(2 * N, -np.finfo(np.float64).max)
     u0 = ops["W0"].copy()  # W0 + Sbar 0 + Ku 0 (:43)
@@ -101,14 +115,13 @@ def main():
     U_d = U0_d.clone()
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
-    gathered = [torch.empty_like(U_d) for _ in range(world)] if (world > 1 and rank == 0) else None
+    gathered = [torch.empty_like(U_d) for _ in range(world)] if rank == 0 else None
 
     def step():
         U_d.copy_(U0_d)          # every step: the reference's first control step of each plant
         solver.reset_state()     # post-setup solver state (x = z = y = 0, rho = settings.rho)
         solver.mpc_step_device(X_d.data_ptr(), U_d.data_ptr(), plant["xref"], sptr)
-        if world > 1:
-            dist.gather(U_d, gathered, dst=0)
+        mdist.gather_moves(dist, U_d, world, rank, gathered)
 
     for _ in range(a.warmup):
         step()
@@ -124,8 +137,7 @@ def main():
         ev[i][0].record(stream)
         solver.mpc_step_device(X_d.data_ptr(), U_d.data_ptr(), plant["xref"], sptr)
         ev[i][1].record(stream)
-        if world > 1:
-            dist.gather(U_d, gathered, dst=0)
+        mdist.gather_moves(dist, U_d, world, rank, gathered)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -163,10 +175,12 @@ def main():
         "config": {"workload": f"cfg2: {B} identical LTI plants per GPU, N={N} (n={N}, m={2 * N}), "
                                f"one controllerStep each", "batch_per_gpu": B, "horizon": N,
                    "parallelism": f"dp{world}"},
-        "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_TFLOPS[a.dtype], "unit": "TFLOP/s",
-                     "frac": achieved / PEAK_TFLOPS[a.dtype], "traffic": None,
-                     "kernel_ms": kern_ms, "flops_per_launch": flops,
-                     "note": "ADMM kernel (admm_lane_kernel) is FP VALU-bound; HBM bytes/QP ~ 300"},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS[a.dtype], "unit": "TFLOP/s",
+                     "frac": achieved / PEAK_TFLOPS[a.dtype], "traffic": traffic_per_solve(a.dtype, B, N),
+                     "kernel": "admm_tile_kernel (all phase launches of one solve)",
+                     "kernel_ms": kern_ms, "flops_per_solve": flops,
+                     "flops_note": "algorithmic: sum over QPs of iters*F_iter + checks*F_check + front end "
+                                   "(SURVEY §8d, DESIGN §4.1), actual per-QP iteration counts"},
         "iters": {"mean": float(iters.mean()), "max": int(iters.max()), "solved_frac": solved},
     }
     if a.cpu_seconds > 0:

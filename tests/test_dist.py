@@ -1,0 +1,68 @@
+"""The N > 1 path on CPU: two gloo ranks each solve their own block of the global counter-based
+stream (oracle as the per-rank solver) and gather the applied moves to rank 0 with the same helpers
+bench.py uses (solvempc_amd.dist).  Rank 0 must hold exactly the single-process result."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+from solvempc_amd import dist as mdist
+from solvempc_amd import workload
+
+N, PER_RANK, WORLD = 20, 48, 2
+
+
+def _moves(start, count):
+    plant = workload.reference_plant()
+    ops = oracle.condense(plant, N)
+    X, U = workload.mpc_states(1, start, count)
+    q, u = oracle.gradient(ops, X, U), oracle.upper_bound(ops, X, U)
+    l = np.full(2 * N, -np.finfo(np.float64).max)
+    x, st, _, _ = oracle.batch_solve(ops["P"], ops["A"], np.zeros(N), l, oracle.upper_bound(ops, np.zeros(4), 0.0),
+                                     q, u, nthreads=1)
+    return U + np.where(st == oracle.SOLVED, x[:, 0], 0.0)  # U += x0 (ModelPredictiveControlAPI.cpp:105)
+
+
+def _worker(rank, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD))
+    r, w, _ = mdist.world_from_env()
+    dist.init_process_group("gloo", rank=r, world_size=w)
+    start, count = mdist.weak_block(PER_RANK, r)
+    moves = torch.from_numpy(_moves(start, count))
+    got = mdist.gather_moves(dist, moves, w, r)
+    if r == 0:
+        out.put(torch.cat(got).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_two_rank_gather_equals_single_process():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(res, _moves(0, PER_RANK * WORLD))
+
+
+def test_blocks_tile_the_stream():
+    assert [mdist.strong_block(10, r, 3) for r in range(3)] == [(0, 4), (4, 3), (7, 3)]
+    assert mdist.weak_block(65536, 3) == (196608, 65536)
+    # counter-based states are shard-invariant
+    a = np.concatenate([workload.mpc_states(1, s, c)[0] for s, c in (mdist.strong_block(100, r, 4) for r in range(4))])
+    np.testing.assert_array_equal(a, workload.mpc_states(1, 0, 100)[0])
