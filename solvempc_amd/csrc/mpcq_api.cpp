@@ -493,20 +493,43 @@ static int phase_stops(const mpcq_settings &st, int *stops)
     return np;
 }
 
+static const char *env_kernel()
+{
+    const char *e = std::getenv("MPCQ_KERNEL");  // test hook: "lane", "wave" or "tile"
+    return e ? e : "";
+}
+
+template <typename T>
+static int wave_launch(mpcq_ctx *c, const mpcq::AdmmArgs<T> &a, int grid, hipStream_t s)
+{
+    return std::is_same<T, float>::value
+               ? mpcq_internal_wave_launch_f32((const mpcq::AdmmArgs<float> *)&a, c->nc, c->mc, grid, s)
+               : mpcq_internal_wave_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->nc, c->mc, grid, s);
+}
+
 template <typename T>
 static int launch_args(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s)
 {
+    const int B = c->dims.batch;
     if (!c->tile) {
-        const int rc = std::is_same<T, float>::value
-                           ? mpcq_internal_admm_launch_f32((const mpcq::AdmmArgs<float> *)&a, c->nc, c->mc, s)
-                           : mpcq_internal_admm_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->nc, c->mc, s);
-        return rc;
+        // per-plant batches: one QP per wave (operators in VGPRs); the lane kernel for shapes the wave
+        // kernel does not compile (n > 32 or m > 64) or when forced by the test hook
+        if (std::strcmp(env_kernel(), "lane") != 0 && c->dims.n <= 32 && c->dims.m <= 64) {
+            a.stop_iter = c->set.max_iter;
+            return wave_launch<T>(c, a, B, s);
+        }
+        return std::is_same<T, float>::value
+                   ? mpcq_internal_admm_launch_f32((const mpcq::AdmmArgs<float> *)&a, c->nc, c->mc, s)
+                   : mpcq_internal_admm_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->nc, c->mc, s);
     }
     int stops[kMaxPhases];
     const int np = phase_stops(c->set, stops);
     if (hipMemsetAsync(c->d_counts, 0, 4 * kMaxPhases, s) != hipSuccess) return -2;
-    const int B = c->dims.batch;
     const int mpc = a.mpc;
+    // phases whose QPs are few (the slow tail) run one QP per wave
+    const char *te = std::getenv("MPCQ_TAIL_PHASE");
+    const bool all_wave = std::strcmp(env_kernel(), "wave") == 0;
+    const int tail_from = all_wave ? 0 : (te ? std::atoi(te) : 3);
     for (int p = 0; p < np; p++) {
         a.img = (const T *)c->d_img;
         a.list_in = p ? c->d_list + (size_t)(p % 2) * B : nullptr;
@@ -517,9 +540,13 @@ static int launch_args(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s)
         a.stop_iter = stops[p];
         a.resume = p > 0;
         a.mpc = p == 0 ? mpc : 0;  // later phases read q, u from the buffers phase 0 filled
-        const int rc = std::is_same<T, float>::value
-                           ? mpcq_internal_tile_launch_f32((const mpcq::AdmmArgs<float> *)&a, c->KN, c->KM, s)
-                           : mpcq_internal_tile_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->KN, c->KM, s);
+        int rc;
+        if (p >= tail_from && c->dims.n <= 32 && c->dims.m <= 64)
+            rc = wave_launch<T>(c, a, p == 0 ? B : std::min(B, 2048), s);
+        else
+            rc = std::is_same<T, float>::value
+                     ? mpcq_internal_tile_launch_f32((const mpcq::AdmmArgs<float> *)&a, c->KN, c->KM, s)
+                     : mpcq_internal_tile_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->KN, c->KM, s);
         if (rc) return rc;
     }
     return 0;

@@ -210,6 +210,10 @@ int mpcq_internal_warm_f32(const mpcq::AdmmArgs<float> *a, int nc, int mc, const
 int mpcq_internal_tile_supported(int KN, int KM);
 int mpcq_internal_tile_launch_f64(const mpcq::AdmmArgs<double> *a, int KN, int KM, hipStream_t s);
 int mpcq_internal_tile_launch_f32(const mpcq::AdmmArgs<float> *a, int KN, int KM, hipStream_t s);
+// One-QP-per-wave path (mpcq_wave.h): grid blocks of 64 threads stride over the (listed) QPs;
+// -1 = n > 32 or m > 64 (not compiled).
+int mpcq_internal_wave_launch_f64(const mpcq::AdmmArgs<double> *a, int nc, int mc, int grid, hipStream_t s);
+int mpcq_internal_wave_launch_f32(const mpcq::AdmmArgs<float> *a, int nc, int mc, int grid, hipStream_t s);
 // Build the TileLayout images (type T = f32 if is_f32) of plant 0 from its fp64 operator block.
 int mpcq_internal_tile_images(const double *ops, int nc, int mc, int KN, int KM, int is_f32, void *img,
                               hipStream_t s);

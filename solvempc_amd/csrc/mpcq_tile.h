@@ -407,9 +407,8 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
                 T zn = tt_fma(rij, y[s], v);
                 if (!LFREE) zn = __builtin_fmax(zn, lh[s]);  // == OSQP's c_max/c_min, NaN included
                 zn = __builtin_fmin(zn, uh[s]);
-                const T d = rj * (v - zn);
-                if (DELTA) dy[s] = d;
-                y[s] = y[s] + d;
+                if (DELTA) dy[s] = rj * (v - zn);  // OSQP delta_y (certificates only)
+                y[s] = tt_fma(rj, v - zn, y[s]);
                 z[s] = zn;
             }
         };

@@ -19,10 +19,11 @@ pytestmark = pytest.mark.gpu
 LMIN = -np.finfo(np.float64).max
 
 
-@pytest.fixture(params=["tile", "lane"])
+@pytest.fixture(params=["tile", "wave", "lane"])
 def kernel(request):
-    """Run a test on both device paths: the MFMA tile kernel (shared plant, the default) and the
-    per-lane kernel (per-plant batches; forced here through the MPCQ_KERNEL test hook)."""
+    """Run a test on every device path: the MFMA tile kernel (shared plant, the default; its tail
+    phases run one QP per wave), the one-QP-per-wave kernel (per-plant batches) and the per-lane
+    kernel (the first kernel), the latter two forced through the MPCQ_KERNEL test hook."""
     old = os.environ.get("MPCQ_KERNEL")
     os.environ["MPCQ_KERNEL"] = request.param
     yield request.param
@@ -297,3 +298,22 @@ def test_dual_infeasible(kernel):
     ref.solve()
     assert ref.info().status == sm.DUAL_INFEASIBLE
     assert np.all(st == sm.DUAL_INFEASIBLE) and np.all(it == ref.info().iter)
+
+
+def test_tile_and_wave_paths_agree(plant):
+    """A QP may move from a tile launch to a wave launch at a phase boundary: both kernels run the
+    same arithmetic in the same order, so whole solves agree (fp32 and fp64)."""
+    N = 20
+    ops, X, U, q, u = _problem(plant, N, 2048, seed=21)
+    for dtype, tol in (("f64", 1e-12), ("f32", 1e-5)):
+        res = {}
+        for k in ("tile", "wave"):
+            os.environ["MPCQ_KERNEL"] = k
+            try:
+                s = _gpu_solve(ops, q, u, N, dtype=dtype)
+                res[k] = (s.solution(), *s.info())
+            finally:
+                os.environ.pop("MPCQ_KERNEL", None)
+        assert np.array_equal(res["tile"][2], res["wave"][2])  # iterations
+        assert np.array_equal(res["tile"][1], res["wave"][1])  # status
+        assert np.abs(res["tile"][0] - res["wave"][0]).max() <= tol

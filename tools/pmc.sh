@@ -14,9 +14,9 @@ while read -r set; do
   rc=$?; echo "pass $i ($set) rc=$rc" >> "$out/passes.txt"
   if [ $rc -ne 0 ]; then exit $rc; fi
 done <<SETS
-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY
+${PMC_SETS:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY
 SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE GRBM_COUNT
 FETCH_SIZE
-WRITE_SIZE
+WRITE_SIZE}
 SETS
 exit 0
