@@ -480,12 +480,24 @@ static int phase_stops(const mpcq_settings &st, int *stops)
 {
     const int ct = st.check_termination;
     int np = 0;
-    const char *e = std::getenv("MPCQ_PHASES");  // test/benchmark hook: "0" = one launch per solve
-    if (ct > 0 && !(e && e[0] == '0')) {
-        static const int mult[] = {3, 4, 5, 6, 8, 12, 20, 40, 80, 160};
-        for (int k : mult) {
-            const long it = (long)k * ct;
+    const char *e = std::getenv("MPCQ_PHASES");  // test/benchmark hook: "0" = one launch per solve,
+                                                  // or a comma list of check multiples ("3,4,5,6,8")
+    int mult[kMaxPhases] = {3, 4, 5, 6, 8, 12, 20, 40, 80, 160};
+    int nm = 10;
+    if (e && e[0] == '0') nm = 0;
+    else if (e && *e) {
+        nm = 0;
+        for (const char *p = e; *p && nm < kMaxPhases - 1;) {
+            mult[nm++] = std::atoi(p);
+            while (*p && *p != ',') p++;
+            if (*p == ',') p++;
+        }
+    }
+    if (ct > 0) {
+        for (int i = 0; i < nm; i++) {
+            const long it = (long)mult[i] * ct;
             if (it >= st.max_iter || np >= kMaxPhases - 1) break;
+            if (np && it <= stops[np - 1]) continue;
             stops[np++] = (int)it;
         }
     }
@@ -530,6 +542,7 @@ static int launch_args(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s)
     const char *te = std::getenv("MPCQ_TAIL_PHASE");
     const bool all_wave = std::strcmp(env_kernel(), "wave") == 0;
     const int tail_from = all_wave ? 0 : (te ? std::atoi(te) : 3);
+
     for (int p = 0; p < np; p++) {
         a.img = (const T *)c->d_img;
         a.list_in = p ? c->d_list + (size_t)(p % 2) * B : nullptr;
@@ -541,9 +554,13 @@ static int launch_args(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s)
         a.resume = p > 0;
         a.mpc = p == 0 ? mpc : 0;  // later phases read q, u from the buffers phase 0 filled
         int rc;
-        if (p >= tail_from && c->dims.n <= 32 && c->dims.m <= 64)
+        if (p >= tail_from && c->dims.n <= 32 && c->dims.m <= 64) {
+            // one QP per wave carries no idle columns: the rest of the solve is one launch
+            a.stop_iter = c->set.max_iter;
             rc = wave_launch<T>(c, a, p == 0 ? B : std::min(B, 2048), s);
-        else
+            if (rc) return rc;
+            break;
+        } else
             rc = std::is_same<T, float>::value
                      ? mpcq_internal_tile_launch_f32((const mpcq::AdmmArgs<float> *)&a, c->KN, c->KM, s)
                      : mpcq_internal_tile_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->KN, c->KM, s);

@@ -153,23 +153,60 @@ __device__ __forceinline__ void tile_mv(const T *__restrict__ im, const T (&x)[X
         for (int r = 0; r < 4; r++) y[4 * t + r] = acc[t][r];
 }
 
-// OCC: waves per SIMD the register allocation is held to (256-thread workgroups).
-template <typename T, int KN, int KM, bool ALL_INEQ, bool LFREE, int OCC>
+// The same product for G independent 16-QP groups of one wave: every A operand read from LDS feeds
+// G MFMAs, and the G accumulator chains interleave (more independent work per wave).
+template <typename T, int G, int NTO, int KS, int KSP, int XN>
+__device__ __forceinline__ void tile_mv_g(const T *__restrict__ im, const T (&x)[G][XN], T (&y)[G][4 * NTO],
+                                          int lane, const T (*init)[4 * NTO])
+{
+    using A = typename Mf<T>::acc;
+    constexpr int VEC = 16 / sizeof(T);
+    constexpr int NG = (KS + VEC - 1) / VEC;
+    typedef T vec __attribute__((ext_vector_type(VEC)));
+    im = fresh_ptr(im);
+    vec opnd[NTO][NG];
+#pragma unroll
+    for (int t = 0; t < NTO; t++)
+#pragma unroll
+        for (int q = 0; q < NG; q++) opnd[t][q] = *(const vec *)(im + TileLayout::at(KSP, VEC, t, q * VEC, lane));
+    A acc[G][NTO];
+#pragma unroll
+    for (int gi = 0; gi < G; gi++)
+#pragma unroll
+        for (int t = 0; t < NTO; t++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) acc[gi][t][r] = init ? init[gi][4 * t + r] : T(0);
+#pragma unroll
+    for (int s = 0; s < KS; s++)
+#pragma unroll
+        for (int t = 0; t < NTO; t++)
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) acc[gi][t] = Mf<T>::mma(opnd[t][s / VEC][s % VEC], x[gi][s], acc[gi][t]);
+#pragma unroll
+    for (int gi = 0; gi < G; gi++)
+#pragma unroll
+        for (int t = 0; t < NTO; t++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) y[gi][4 * t + r] = acc[gi][t][r];
+}
+
+// G: 16-QP groups per wave; OCC: waves per SIMD the register allocation is held to (256-thread
+// workgroups, so one workgroup carries 64 G QPs).
+template <typename T, int KN, int KM, bool ALL_INEQ, bool LFREE, int G, int OCC>
 __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
 {
     constexpr int VEC = 16 / sizeof(T);
     constexpr TileLayout L = TileLayout::make(KN, KM, VEC);
     constexpr int NT = L.NT, MT = L.MT, KNP = L.KNP, KMP = L.KMP;
     constexpr int NS = 4 * NT, MS = 4 * MT;  // registers per n- / m-vector
-    constexpr int is32 = sizeof(T) == 4;
-    (void)is32;
     constexpr int NCP = 16 * NT, MCP = 16 * MT;  // padded row counts (== ctx nc, mc)
+    constexpr int QPW = 64 * G;                  // QPs per workgroup
     __shared__ __attribute__((aligned(16))) T img[L.total];
     __shared__ T rowv[3 * NCP + 2 * MCP];        // lam, D, Dinv | E, Einv of the plant
     T *const s_lam = rowv, *const s_D = rowv + NCP, *const s_Dinv = rowv + 2 * NCP;
     T *const s_E = rowv + 3 * NCP, *const s_Einv = rowv + 3 * NCP + MCP;
     const int count = a.count_in ? *a.count_in : a.batch;
-    if (blockIdx.x * 64 >= count) return;  // whole workgroup idle in this phase (uniform)
+    if (blockIdx.x * QPW >= count) return;  // whole workgroup idle in this phase (uniform)
     for (int i = threadIdx.x; i < NCP; i += 256) {
         s_lam[i] = a.ops.lam[i];
         s_D[i] = a.ops.D[i];
@@ -190,170 +227,209 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
     __syncthreads();  // the only barrier: waves are independent from here on
 
     const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-    const int wave_slot = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+    const int wave_slot = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 * G;
     if (wave_slot >= count) return;
-    const bool valid = wave_slot + c < count;
-    const int b_ = valid ? (a.list_in ? a.list_in[wave_slot + c] : wave_slot + c) : 0;
-    int b = b_;
+    bool valid[G];
+    int b_[G];
+#pragma unroll
+    for (int gi = 0; gi < G; gi++) {
+        const int slot = wave_slot + 16 * gi + c;
+        valid[gi] = slot < count;
+        b_[gi] = valid[gi] ? (a.list_in ? a.list_in[slot] : slot) : 0;
+    }
     const int n = a.n, m = a.m;
-    const int ncs = 4 * NT * 4, mcs = 4 * MT * 4;  // state row strides (ctx nc = 16 NT, mc = 16 MT)
+    const int ncs = NCP, mcs = MCP;                // state row strides (ctx nc, mc)
     const PlantOps<T> op = a.ops;                  // shared plant: block 0
     const int *ctype = a.ctype;
     const SolverSettings &st = a.st;
     const bool scaled_term = st.scaled_termination != 0;
     const double c64 = (double)op.cs[0];
 
-    // ---- per-QP data (element v = 4 s + g of this lane's QP column)
-    double Xv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    double Uv = 0.0;
-    if (a.mpc) {
+    // ---- per-QP data (element v = 4 s + g of this lane's QP column), per group
+    T qh[G][NS];  // q^ = c D q (osqp_update_lin_cost), kept for the dual residual
+    T uh[G][MS], lh[G][LFREE ? 1 : MS];
+    T rs[ALL_INEQ ? 1 : MS];
+    int status[G];
 #pragma unroll
-        for (int t = 0; t < 8; t++)
-            if (t < a.nx) Xv[t] = a.X[(size_t)b * a.nx + t];
-    }
-    if (a.mpc_u) Uv = a.U[b];
-    T qh[NS];  // q^ = c D q (osqp_update_lin_cost), kept for the dual residual
+    for (int gi = 0; gi < G; gi++) {
+        const int b = b_[gi];
+        double Xv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        double Uv = 0.0;
+        if (a.mpc) {
 #pragma unroll
-    for (int s = 0; s < NS; s++) {
-        const int v = 4 * s + g;
-        double qk = 0.0;
-        if (s < KN && v < n) {
-            if (a.mpc) {  // setF (:372-375): q = Fx X + Fu U + Fr ref
-                const double *fx = a.Fx + (size_t)v * a.nx;
-                const double *fr = a.Fr + (size_t)v * n;
-                double s0 = 0.0, s2 = 0.0;
-#pragma unroll
-                for (int t = 0; t < 8; t++)
-                    if (t < a.nx) s0 += fx[t] * Xv[t];
-                const double s1 = a.Fu[v] * Uv;
-                for (int t = 0; t < n; t++) s2 += fr[t] * a.xref;
-                qk = s0 + s1 + s2;
-                if (valid) a.q_out[(size_t)b * n + v] = qk;
-            } else {
-                qk = a.q[(size_t)b * n + v];
-            }
+            for (int t = 0; t < 8; t++)
+                if (t < a.nx) Xv[t] = a.X[(size_t)b * a.nx + t];
+            Uv = a.U[b];
         }
-        qh[s] = s < KN ? (T)((qk * (double)op.D[s < KN ? v : 0]) * c64) : T(0);  // osqp_update_lin_cost
-    }
-    int bad = 0, tchg = 0;
-    T uh[MS], lh[LFREE ? 1 : MS], rs[ALL_INEQ ? 1 : MS];
 #pragma unroll
-    for (int s = 0; s < MS; s++) {
-        const int v = 4 * s + g;
-        double up = kInfty, lo = -kInfty;
-        if (s < KM && v < m) {
-            if (a.mpc) {  // setUpperBound (:360-369) + :99: u = W0 + Sbar X + Ku U
-                const double *sb = a.Sbar + (size_t)v * a.nx;
-                double sx = 0.0;
+        for (int s = 0; s < NS; s++) {
+            const int v = 4 * s + g;
+            double qk = 0.0;
+            if (s < KN && v < n) {
+                if (a.mpc) {  // setF (:372-375): q = Fx X + Fu U + Fr ref
+                    const double *fx = a.Fx + (size_t)v * a.nx;
+                    const double *fr = a.Fr + (size_t)v * n;
+                    double s0 = 0.0, s2 = 0.0;
 #pragma unroll
-                for (int t = 0; t < 8; t++)
-                    if (t < a.nx) sx += sb[t] * Xv[t];
-                up = a.W0[v] + sx + a.Ku[v] * Uv;
-                if (valid) a.u_out[(size_t)b * m + v] = up;
-            } else {
-                up = a.u[(size_t)b * m + v];
+                    for (int t = 0; t < 8; t++)
+                        if (t < a.nx) s0 += fx[t] * Xv[t];
+                    const double s1 = a.Fu[v] * Uv;
+                    for (int t = 0; t < n; t++) s2 += fr[t] * a.xref;
+                    qk = s0 + s1 + s2;
+                    if (valid[gi]) a.q_out[(size_t)b * n + v] = qk;
+                } else {
+                    qk = a.q[(size_t)b * n + v];
+                }
             }
-            lo = a.l[(a.l_shared ? 0 : (size_t)b * m) + v];
-            const double e = (double)op.E[v];  // osqp_update_bounds: u^ = E u, l^ = E l
-            up *= e;
-            lo *= e;
-            if (up < lo) bad = 1;
-            const int ty = (lo < -kInfty * kMinScaling && up > kInfty * kMinScaling) ? -1 : (up - lo < kRhoTol ? 1 : 0);
-            if (ty != ctype[v]) tchg = 1;
-            if (LFREE && !((T)lo < T(-kInfty * kMinScaling))) tchg = 1;
+            qh[gi][s] = s < KN ? (T)((qk * (double)op.D[s < KN ? v : 0]) * c64) : T(0);
         }
-        uh[s] = (T)up;
-        if (!LFREE) lh[s] = (T)lo;
-        if (!ALL_INEQ) rs[s] = (s < KM && v < m) ? (ctype[v] == -1 ? T(-1) : op.rscale[v]) : T(1);
+        int bad = 0, tchg = 0;
+#pragma unroll
+        for (int s = 0; s < MS; s++) {
+            const int v = 4 * s + g;
+            double up = kInfty, lo = -kInfty;
+            if (s < KM && v < m) {
+                if (a.mpc) {  // setUpperBound (:360-369) + :99: u = W0 + Sbar X + Ku U
+                    const double *sb = a.Sbar + (size_t)v * a.nx;
+                    double sx = 0.0;
+#pragma unroll
+                    for (int t = 0; t < 8; t++)
+                        if (t < a.nx) sx += sb[t] * Xv[t];
+                    up = a.W0[v] + sx + a.Ku[v] * Uv;
+                    if (valid[gi]) a.u_out[(size_t)b * m + v] = up;
+                } else {
+                    up = a.u[(size_t)b * m + v];
+                }
+                lo = a.l[(a.l_shared ? 0 : (size_t)b * m) + v];
+                const double e = (double)op.E[v];  // osqp_update_bounds: u^ = E u, l^ = E l
+                up *= e;
+                lo *= e;
+                if (up < lo) bad = 1;
+                const int ty = (lo < -kInfty * kMinScaling && up > kInfty * kMinScaling) ? -1 : (up - lo < kRhoTol ? 1 : 0);
+                if (ty != ctype[v]) tchg = 1;
+                if (LFREE && !((T)lo < T(-kInfty * kMinScaling))) tchg = 1;
+            }
+            uh[gi][s] = (T)up;
+            if (!LFREE) lh[gi][s] = (T)lo;
+            if (!ALL_INEQ && gi == 0) rs[s] = (s < KM && v < m) ? (ctype[v] == -1 ? T(-1) : op.rscale[v]) : T(1);
+        }
+        bad = col_or(bad);
+        tchg = col_or(tchg);
+        status[gi] = bad ? kInvalidBounds : (tchg ? kTypeChanged : kUnsolved);
     }
-    bad = col_or(bad);
-    tchg = col_or(tchg);
-    int status = bad ? kInvalidBounds : (tchg ? kTypeChanged : kUnsolved);
 
     // g = W' q^ (the q-part of the KKT right-hand side in the W-basis)
-    T gv[NS];
-    tile_mv<T, NT, KN, KNP>(img + L.Wt, qh, gv, lane, (const T *)nullptr);
+    T gv[G][NS];
+    tile_mv_g<T, G, NT, KN, KNP>(img + L.Wt, qh, gv, lane, nullptr);
 #pragma unroll
-    for (int s = 0; s < NS; s++) gv[s] = s < KN ? -gv[s] : T(0);  // xi starts from -g (padding rows 0)
+    for (int gi = 0; gi < G; gi++)
+#pragma unroll
+        for (int s = 0; s < NS; s++) gv[gi][s] = s < KN ? -gv[gi][s] : T(0);  // xi starts from -g
 
     // ---- state: x' (W-basis), z, y; rho persists across solves (OSQP)
-    T xs[NS], z[MS], y[MS];
-    T rho;
+    T xs[G][NS], z[G][MS], y[G][MS];
+    T rho[G], rinv[G];
     int it = 0;
     const bool load_state = a.resume || (a.warm && !a.fresh);
-    if (a.resume) {
-        rho = a.rhos[b];
-        it = a.it_state[b];
-    } else {
-        rho = a.fresh ? (T)fmin(fmax(st.rho, kRhoMin), kRhoMax) : a.rhos[b];
-    }
 #pragma unroll
-    for (int s = 0; s < NS; s++) xs[s] = (load_state && s < KN) ? a.xs[(size_t)b * ncs + 4 * s + g] : T(0);
+    for (int gi = 0; gi < G; gi++) {
+        const int b = b_[gi];
+        if (a.resume) {
+            rho[gi] = a.rhos[b];
+            if (gi == 0) it = a.it_state[b];
+        } else {
+            rho[gi] = a.fresh ? (T)fmin(fmax(st.rho, kRhoMin), kRhoMax) : a.rhos[b];
+        }
 #pragma unroll
-    for (int s = 0; s < MS; s++) {
-        z[s] = (load_state && s < KM) ? a.zs[(size_t)b * mcs + 4 * s + g] : T(0);
-        y[s] = (load_state && s < KM) ? a.ys[(size_t)b * mcs + 4 * s + g] : T(0);
+        for (int s = 0; s < NS; s++) xs[gi][s] = (load_state && s < KN) ? a.xs[(size_t)b * ncs + 4 * s + g] : T(0);
+#pragma unroll
+        for (int s = 0; s < MS; s++) {
+            z[gi][s] = (load_state && s < KM) ? a.zs[(size_t)b * mcs + 4 * s + g] : T(0);
+            y[gi][s] = (load_state && s < KM) ? a.ys[(size_t)b * mcs + 4 * s + g] : T(0);
+        }
+        rinv[gi] = T(1) / rho[gi];
     }
     it = __builtin_amdgcn_readfirstlane(it);  // lane 0 is always a live column; a phase shares `it`
-    T rinv = T(1) / rho;
-    T dk[NS];
+    T dk[G][NS];
     auto set_dk = [&]() {
         const T *lam = fresh_ptr((const T *)s_lam);
 #pragma unroll
-        for (int s = 0; s < NS; s++) dk[s] = T(1) / (T(1) + rho * lam[4 * s + g]);  // lam padded with 0
+        for (int gi = 0; gi < G; gi++)
+#pragma unroll
+            for (int s = 0; s < NS; s++) dk[gi][s] = T(1) / (T(1) + rho[gi] * lam[4 * s + g]);  // lam padded 0
     };
     set_dk();
 
     const T alpha = (T)st.alpha, oma = T(1) - (T)st.alpha;
     const T eps_abs = (T)st.eps_abs, eps_rel = (T)st.eps_rel;
-    bool done = !valid;
+    bool done[G];
+#pragma unroll
+    for (int gi = 0; gi < G; gi++) done[gi] = !valid[gi];
 
-    // ---- write one QP's results (OSQP store_solution / update_info; warm-start state)
-    auto finalize = [&](bool mine) {
-        const int b = opaque(b_);
+    // ---- write the results of the `mine` QPs (OSQP store_solution / update_info; warm-start state)
+    auto finalize = [&](const bool (&mine)[G]) {
         // x = D W x'  (all lanes run the MFMA; `mine` lanes store)
-        T xh[NS];
-        tile_mv<T, NT, KN, KNP>(img + L.W, xs, xh, lane, (const T *)nullptr);
-        if (!mine) return;
-        const bool has_sol = status == kSolved || status == kSolvedInaccurate || status == kMaxIterReached;
+        T xh[G][NS];
+        tile_mv_g<T, G, NT, KN, KNP>(img + L.W, xs, xh, lane, nullptr);
         const double cinv64 = (double)op.cs[1];
 #pragma unroll
-        for (int s = 0; s < NS; s++) {
-            const int v = 4 * s + g;
-            if (s < KN && v < n) {
-                const double xv = has_sol ? (double)xh[s] * (double)s_D[v] : __builtin_nan("");
-                if (a.x) a.x[(size_t)b * n + v] = xv;
-                if (v == 0 && a.mpc_u && status == kSolved) a.U[b] = a.U[b] + xv;  // U += x(0)  (:105)
+        for (int gi = 0; gi < G; gi++) {
+            if (!mine[gi]) continue;
+            const int b = opaque(b_[gi]);
+            const int sta = status[gi];
+            const bool has_sol = sta == kSolved || sta == kSolvedInaccurate || sta == kMaxIterReached;
+#pragma unroll
+            for (int s = 0; s < NS; s++) {
+                const int v = 4 * s + g;
+                if (s < KN && v < n) {
+                    const double xv = has_sol ? (double)xh[gi][s] * (double)s_D[v] : __builtin_nan("");
+                    if (a.x) a.x[(size_t)b * n + v] = xv;
+                    if (v == 0 && a.mpc_u && sta == kSolved) a.U[b] = a.U[b] + xv;  // U += x(0)  (:105)
+                }
             }
-        }
 #pragma unroll
-        for (int s = 0; s < MS; s++) {
-            const int v = 4 * s + g;
-            if (s < KM && v < m && a.y)
-                a.y[(size_t)b * m + v] = has_sol ? ((double)y[s] * (double)s_E[v]) * cinv64 : __builtin_nan("");
-        }
-        const bool keep = has_sol || status == kInvalidBounds || status == kTypeChanged;
-#pragma unroll
-        for (int s = 0; s < NS; s++)
-            if (s < KN) a.xs[(size_t)b * ncs + 4 * s + g] = keep ? xs[s] : T(0);
-#pragma unroll
-        for (int s = 0; s < MS; s++)
-            if (s < KM) {
-                a.zs[(size_t)b * mcs + 4 * s + g] = keep ? z[s] : T(0);
-                a.ys[(size_t)b * mcs + 4 * s + g] = keep ? y[s] : T(0);
+            for (int s = 0; s < MS; s++) {
+                const int v = 4 * s + g;
+                if (s < KM && v < m && a.y)
+                    a.y[(size_t)b * m + v] = has_sol ? ((double)y[gi][s] * (double)s_E[v]) * cinv64 : __builtin_nan("");
             }
-        if (g == 0) {
-            a.rhos[b] = rho;
-            a.status[b] = status;
-            a.iter[b] = it;
-            a.rho_out[b] = (double)rho;
+            const bool keep = has_sol || sta == kInvalidBounds || sta == kTypeChanged;
+#pragma unroll
+            for (int s = 0; s < NS; s++)
+                if (s < KN) a.xs[(size_t)b * ncs + 4 * s + g] = keep ? xs[gi][s] : T(0);
+#pragma unroll
+            for (int s = 0; s < MS; s++)
+                if (s < KM) {
+                    a.zs[(size_t)b * mcs + 4 * s + g] = keep ? z[gi][s] : T(0);
+                    a.ys[(size_t)b * mcs + 4 * s + g] = keep ? y[gi][s] : T(0);
+                }
+            if (g == 0) {
+                a.rhos[b] = rho[gi];
+                a.status[b] = sta;
+                a.iter[b] = it;
+                a.rho_out[b] = (double)rho[gi];
+            }
         }
     };
+    auto all_done = [&]() {
+        bool d = true;
+#pragma unroll
+        for (int gi = 0; gi < G; gi++) d = d && done[gi];
+        return wave_all(d);
+    };
 
-    if (wave_any(valid && status != kUnsolved)) {
-        const bool mine = valid && status != kUnsolved;
-        finalize(mine);
-        done = done || mine;
+    {
+        bool mine[G], any = false;
+#pragma unroll
+        for (int gi = 0; gi < G; gi++) {
+            mine[gi] = valid[gi] && status[gi] != kUnsolved;
+            any = any || mine[gi];
+        }
+        if (wave_any(any)) {
+            finalize(mine);
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) done[gi] = done[gi] || mine[gi];
+        }
     }
 
     const int ct = st.check_termination;
@@ -361,7 +437,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
     const int stop = a.stop_iter;
     int next_check = ct ? (it / ct + 1) * ct : -1;  // uniform; no integer division in the loop
     int next_adapt = ai ? (it / ai + 1) * ai : -1;
-    while (!wave_all(done)) {
+    while (!all_done()) {
         it++;
         const bool at_check = it == next_check;
         const bool at_adapt = it == next_adapt;
@@ -372,45 +448,51 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
 
         // ---- one ADMM iteration; the check iterations also keep delta_x', delta_y (OSQP's
         // delta_x / delta_y, for the infeasibility certificates)
-        T dx[NS], dy[MS];
+        T dx[G][NS], dy[G][MS];
         auto iterate = [&](auto with_delta) {
             constexpr bool DELTA = decltype(with_delta)::value;
             // xi = -g + sigma W'W x' + B' w,   w_j = rho_j z_j - y_j   (w reuses the zt registers)
-            T wz[MS];
+            T wz[G][MS];
 #pragma unroll
-            for (int s = 0; s < MS; s++) {
-                T rj = rho;
-                if (!ALL_INEQ) rj = rs[s] < T(0) ? T(kRhoMin) : rho * rs[s];
-                wz[s] = s < KM ? tt_fma(rj, z[s], -y[s]) : T(0);
-            }
-            T xi[NS];
-            tile_mv<T, NT, KN, KNP>(img + L.S, xs, xi, lane, gv);   // xi = -g + S x'
-            tile_mv<T, NT, KM, KMP>(img + L.Bt, wz, xi, lane, xi);  //    + B' w
+            for (int gi = 0; gi < G; gi++)
+#pragma unroll
+                for (int s = 0; s < MS; s++) {
+                    T rj = rho[gi];
+                    if (!ALL_INEQ) rj = rs[s] < T(0) ? T(kRhoMin) : rho[gi] * rs[s];
+                    wz[gi][s] = s < KM ? tt_fma(rj, z[gi][s], -y[gi][s]) : T(0);
+                }
+            T xi[G][NS];
+            tile_mv_g<T, G, NT, KN, KNP>(img + L.S, xs, xi, lane, gv);   // xi = -g + S x'
+            tile_mv_g<T, G, NT, KM, KMP>(img + L.Bt, wz, xi, lane, xi);  //    + B' w
             // eta = xi / (1 + rho lambda) ; x' = alpha eta + (1 - alpha) x'
 #pragma unroll
-            for (int s = 0; s < KN; s++) {  // registers s >= KN are padding rows: x' stays 0 there
-                xi[s] = xi[s] * dk[s];
-                const T xn = tt_fma(alpha, xi[s], oma * xs[s]);
-                if (DELTA) dx[s] = xn - xs[s];
-                xs[s] = xn;
-            }
-            // z~ = B eta ; relaxation ; projection ; dual update
-            tile_mv<T, MT, KN, KNP>(img + L.B, xi, wz, lane, (const T *)nullptr);
+            for (int gi = 0; gi < G; gi++)
 #pragma unroll
-            for (int s = 0; s < KM; s++) {
-                T rj = rho, rij = rinv;
-                if (!ALL_INEQ) {
-                    rj = rs[s] < T(0) ? T(kRhoMin) : rho * rs[s];
-                    rij = T(1) / rj;
+                for (int s = 0; s < KN; s++) {  // registers s >= KN are padding rows: x' stays 0 there
+                    xi[gi][s] = xi[gi][s] * dk[gi][s];
+                    const T xn = tt_fma(alpha, xi[gi][s], oma * xs[gi][s]);
+                    if (DELTA) dx[gi][s] = xn - xs[gi][s];
+                    xs[gi][s] = xn;
                 }
-                const T v = tt_fma(alpha, wz[s], oma * z[s]);
-                T zn = tt_fma(rij, y[s], v);
-                if (!LFREE) zn = __builtin_fmax(zn, lh[s]);  // == OSQP's c_max/c_min, NaN included
-                zn = __builtin_fmin(zn, uh[s]);
-                if (DELTA) dy[s] = rj * (v - zn);  // OSQP delta_y (certificates only)
-                y[s] = tt_fma(rj, v - zn, y[s]);
-                z[s] = zn;
-            }
+            // z~ = B eta ; relaxation ; projection ; dual update
+            tile_mv_g<T, G, MT, KN, KNP>(img + L.B, xi, wz, lane, nullptr);
+#pragma unroll
+            for (int gi = 0; gi < G; gi++)
+#pragma unroll
+                for (int s = 0; s < KM; s++) {
+                    T rj = rho[gi], rij = rinv[gi];
+                    if (!ALL_INEQ) {
+                        rj = rs[s] < T(0) ? T(kRhoMin) : rho[gi] * rs[s];
+                        rij = T(1) / rj;
+                    }
+                    const T v = tt_fma(alpha, wz[gi][s], oma * z[gi][s]);
+                    T zn = tt_fma(rij, y[gi][s], v);
+                    if (!LFREE) zn = __builtin_fmax(zn, lh[gi][s]);  // == OSQP's c_max/c_min, NaN included
+                    zn = __builtin_fmin(zn, uh[gi][s]);
+                    if (DELTA) dy[gi][s] = rj * (v - zn);  // OSQP delta_y (certificates only)
+                    y[gi][s] = tt_fma(rj, v - zn, y[gi][s]);
+                    z[gi][s] = zn;
+                }
         };
         if (!info) {
             iterate(std::false_type{});
@@ -418,221 +500,319 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
         }
         iterate(std::true_type{});
 #pragma unroll
-        for (int s = KM; s < MS; s++) dy[s] = T(0);
+        for (int gi = 0; gi < G; gi++)
+#pragma unroll
+            for (int s = KM; s < MS; s++) dy[gi][s] = T(0);
 
         // ---- update_info: residuals in the scaled space (reported unscaled), 4-lane reductions
-        T ax_z = 0, ax_zs = 0, zn_s = 0, zn_r = 0, axn_s = 0, axn_r = 0;
+        T ax_z[G], ax_zs[G], zn_s[G], zn_r[G], axn_s[G], axn_r[G];
         {
-            T ax[MS];
-            tile_mv<T, MT, KN, KNP>(img + L.B, xs, ax, lane, (const T *)nullptr);
+            T ax[G][MS];
+            tile_mv_g<T, G, MT, KN, KNP>(img + L.B, xs, ax, lane, nullptr);
             const T *Einv = fresh_ptr((const T *)s_Einv);
 #pragma unroll
-            for (int s = 0; s < KM; s++) {
-                const T r = ax[s] - z[s];
-                const T ei = Einv[4 * s + g];
-                ax_z = nrm(ax_z, r);
-                ax_zs = nrm(ax_zs, ei * r);
-                zn_r = nrm(zn_r, z[s]);
-                zn_s = nrm(zn_s, ei * z[s]);
-                axn_r = nrm(axn_r, ax[s]);
-                axn_s = nrm(axn_s, ei * ax[s]);
-            }
-        }
-        T dr_r = 0, dr_s = 0, qn_r = 0, qn_s = 0, atyn_r = 0, atyn_s = 0, pxn_r = 0, pxn_s = 0;
-        {
-            T px[NS], aty[NS];
-            tile_mv<T, NT, KN, KNP>(img + L.PW, xs, px, lane, (const T *)nullptr);
-            tile_mv<T, NT, KM, KMP>(img + L.AhT, y, aty, lane, (const T *)nullptr);
-            const T *Dinv = fresh_ptr((const T *)s_Dinv);
+            for (int gi = 0; gi < G; gi++) {
+                ax_z[gi] = ax_zs[gi] = zn_s[gi] = zn_r[gi] = axn_s[gi] = axn_r[gi] = T(0);
 #pragma unroll
-            for (int s = 0; s < KN; s++) {
-                const T qhs = qh[s];
-                const T r = (qhs + px[s]) + aty[s];
-                const T di = Dinv[4 * s + g];
-                dr_r = nrm(dr_r, r);
-                dr_s = nrm(dr_s, di * r);
-                qn_r = nrm(qn_r, qhs);
-                qn_s = nrm(qn_s, di * qhs);
-                atyn_r = nrm(atyn_r, aty[s]);
-                atyn_s = nrm(atyn_s, di * aty[s]);
-                pxn_r = nrm(pxn_r, px[s]);
-                pxn_s = nrm(pxn_s, di * px[s]);
-            }
-        }
-        ax_z = col_max(ax_z); ax_zs = col_max(ax_zs); zn_s = col_max(zn_s); zn_r = col_max(zn_r);
-        axn_s = col_max(axn_s); axn_r = col_max(axn_r);
-        dr_r = col_max(dr_r); dr_s = col_max(dr_s); qn_r = col_max(qn_r); qn_s = col_max(qn_s);
-        atyn_r = col_max(atyn_r); atyn_s = col_max(atyn_s); pxn_r = col_max(pxn_r); pxn_s = col_max(pxn_s);
-        const T cinv = op.cs[1];
-        const T pri_res = scaled_term ? ax_z : ax_zs;
-        const T dua_res = scaled_term ? dr_r : cinv * dr_s;
-
-        // OSQP is_primal_infeasible on delta_y = dy (this iteration's dual step).
-        auto primal_infeasible = [&](T eps, bool need) -> bool {
-            T d[MS];
-            T ndy = 0, lhs = 0;
-            const T *E = fresh_ptr((const T *)s_E);
-#pragma unroll
-            for (int s = 0; s < MS; s++) {
-                if (s >= KM) { d[s] = T(0); continue; }
-                T dd = dy[s];
-                const T up = uh[s], lo = LFREE ? T(-kInfty) : lh[s];
-                const bool uinf = up > T(kInfty * kMinScaling), linf = lo < T(-kInfty * kMinScaling);
-                if (uinf) dd = linf ? T(0) : tt_min(dd, T(0));
-                else if (linf) dd = tt_max(dd, T(0));
-                d[s] = dd;
-                ndy = nrm(ndy, scaled_term ? dd : E[4 * s + g] * dd);
-                if (up < T(kInfty * kMinScaling)) lhs += up * tt_max(dd, T(0));
-                if (lo > T(-kInfty * kMinScaling)) lhs += lo * tt_min(dd, T(0));
-            }
-            ndy = col_max(ndy);
-            lhs = col_sum(lhs);
-            const bool cand = need && ndy > T(kDivisionTol) && lhs < eps * ndy;
-            if (!wave_any(cand)) return false;
-            T atd[NS];
-            tile_mv<T, NT, KM, KMP>(img + L.AhT, d, atd, lane, (const T *)nullptr);
-            const T *Dinv = fresh_ptr((const T *)s_Dinv);
-            T nat = 0;
-#pragma unroll
-            for (int s = 0; s < KN; s++) nat = nrm(nat, scaled_term ? atd[s] : Dinv[4 * s + g] * atd[s]);
-            nat = col_max(nat);
-            return cand && nat < eps * ndy;
-        };
-        // OSQP is_dual_infeasible on delta_x^ = W dx.
-        auto dual_infeasible = [&](T eps, bool need) -> bool {
-            T qdx = 0;  // q^' dx^ = (W' q^)' dx' = -gv' dx'
-#pragma unroll
-            for (int s = 0; s < KN; s++) qdx = tt_fma(-gv[s], dx[s], qdx);
-            qdx = col_sum(qdx);
-            bool cand = need && qdx < T(0);
-            if (!wave_any(cand)) return false;
-            T t1[NS];
-            tile_mv<T, NT, KN, KNP>(img + L.W, dx, t1, lane, (const T *)nullptr);
-            const T *D = fresh_ptr((const T *)s_D);
-            T ndx = 0;
-#pragma unroll
-            for (int s = 0; s < KN; s++) ndx = nrm(ndx, scaled_term ? t1[s] : D[4 * s + g] * t1[s]);
-            ndx = col_max(ndx);
-            const T cs = scaled_term ? T(1) : op.cs[0];
-            cand = cand && ndx > T(kDivisionTol) && qdx < -cs * eps * ndx;
-            if (!wave_any(cand)) return false;
-            tile_mv<T, NT, KN, KNP>(img + L.PW, dx, t1, lane, (const T *)nullptr);
-            const T *Dinv = fresh_ptr((const T *)s_Dinv);
-            T npdx = 0;
-#pragma unroll
-            for (int s = 0; s < KN; s++) npdx = nrm(npdx, scaled_term ? t1[s] : Dinv[4 * s + g] * t1[s]);
-            npdx = col_max(npdx);
-            cand = cand && npdx < cs * eps * ndx;
-            if (!wave_any(cand)) return false;
-            T adx[MS];
-            tile_mv<T, MT, KN, KNP>(img + L.B, dx, adx, lane, (const T *)nullptr);
-            const T *Einv = fresh_ptr((const T *)s_Einv);
-            int viol = 0;
-#pragma unroll
-            for (int s = 0; s < KM; s++) {
-                const T sv = scaled_term ? adx[s] : Einv[4 * s + g] * adx[s];
-                const T up = uh[s], lo = LFREE ? T(-kInfty) : lh[s];
-                if ((up < T(kInfty * kMinScaling) && sv > eps * ndx) || (lo > T(-kInfty * kMinScaling) && sv < -eps * ndx))
-                    viol = 1;
-            }
-            viol = col_or(viol);
-            return cand && !viol;
-        };
-        // check_termination(approximate) — OSQP auxil.c; returns the new status (kUnsolved: go on)
-        auto check_termination = [&](bool approx, bool need) -> int {
-            const T mul = approx ? T(10) : T(1);
-            const bool noncvx = pri_res > T(kInfty) || dua_res > T(kInfty);
-            need = need && !noncvx;  // every lane runs the (uniform) certificate code below
-            const T ea = eps_abs * mul, er = eps_rel * mul;
-            bool prim_ok = (m == 0), dual_ok = false;
-            bool need_p = false;
-            if (m > 0) {
-                const T ep = ea + er * (scaled_term ? tt_max(zn_r, axn_r) : tt_max(zn_s, axn_s));
-                prim_ok = pri_res < ep;
-                need_p = !prim_ok;
-            }
-            const bool prim_inf = primal_infeasible((T)st.eps_prim_inf * mul, need && need_p);
-            const T ed = ea + er * (scaled_term ? tt_max(tt_max(qn_r, atyn_r), pxn_r)
-                                                : cinv * tt_max(tt_max(qn_s, atyn_s), pxn_s));
-            dual_ok = dua_res < ed;
-            const bool dual_inf = dual_infeasible((T)st.eps_dual_inf * mul, need && !dual_ok);
-            if (noncvx) return kNonCvx;
-            if (prim_ok && dual_ok) return approx ? kSolvedInaccurate : kSolved;
-            if (prim_inf) return approx ? kPrimalInfeasibleInaccurate : kPrimalInfeasible;
-            if (dual_inf) return approx ? kDualInfeasibleInaccurate : kDualInfeasible;
-            return kUnsolved;
-        };
-
-        bool term = done;  // finished (or dead) columns ignore everything below
-        if (at_check) {
-            const int s0 = check_termination(false, !term);
-            if (!term && s0 != kUnsolved) { status = s0; term = true; }
-        }
-        if (at_adapt && !term) {  // adapt_rho / compute_rho_estimate (scaled-space norms)
-            const T pr = ax_z / (tt_max(zn_r, axn_r) + T(kDivisionTol));
-            const T dn = tt_max(tt_max(qn_r, atyn_r), pxn_r);
-            const T du = dr_r / (dn + T(kDivisionTol));
-            T rn = rho * (T)sqrt((double)(pr / (du + T(kDivisionTol))));
-            rn = tt_min(tt_max(rn, T(kRhoMin)), T(kRhoMax));
-            if (rn > rho * (T)st.adaptive_rho_tolerance || rn < rho / (T)st.adaptive_rho_tolerance) {
-                rho = tt_min(tt_max(rn, T(kRhoMin)), T(kRhoMax));
-                rinv = T(1) / rho;
-            }
-        }
-        if (at_adapt) set_dk();  // uniform; unchanged rho gives the same dk bit for bit
-        if (last) {  // after the ADMM loop (osqp_solve)
-            const int s1 = at_check ? kUnsolved : check_termination(false, !term);
-            if (!term && s1 != kUnsolved) { status = s1; term = true; }
-            const int s2 = check_termination(true, !term);
-            if (!term) { status = s2 != kUnsolved ? s2 : kMaxIterReached; term = true; }
-        }
-        const bool newly = term && !done;
-        if (wave_any(newly)) finalize(newly);
-        done = term;
-        if (it == stop && !wave_all(done)) {
-            // phase boundary: save the running QPs and queue them for the next launch
-            const bool run = !done;
-            const int b = opaque(b_);
-            if (run) {
-#pragma unroll
-                for (int s = 0; s < NS; s++)
-                    if (s < KN) a.xs[(size_t)b * ncs + 4 * s + g] = xs[s];
-#pragma unroll
-                for (int s = 0; s < MS; s++)
-                    if (s < KM) {
-                        a.zs[(size_t)b * mcs + 4 * s + g] = z[s];
-                        a.ys[(size_t)b * mcs + 4 * s + g] = y[s];
-                    }
-                if (g == 0) {
-                    a.rhos[b] = rho;
-                    a.it_state[b] = it;
+                for (int s = 0; s < KM; s++) {
+                    const T r = ax[gi][s] - z[gi][s];
+                    const T ei = Einv[4 * s + g];
+                    ax_z[gi] = nrm(ax_z[gi], r);
+                    ax_zs[gi] = nrm(ax_zs[gi], ei * r);
+                    zn_r[gi] = nrm(zn_r[gi], z[gi][s]);
+                    zn_s[gi] = nrm(zn_s[gi], ei * z[gi][s]);
+                    axn_r[gi] = nrm(axn_r[gi], ax[gi][s]);
+                    axn_s[gi] = nrm(axn_s[gi], ei * ax[gi][s]);
                 }
             }
-            const unsigned long long mask = __ballot(run && g == 0);
-            int base = 0;
-            if (lane == 0) base = atomicAdd(a.count_out, __popcll(mask));
-            base = __shfl(base, 0);
-            if (run && g == 0) a.list_out[base + __popcll(mask & ((1ull << lane) - 1ull))] = b;
+        }
+        T dr_r[G], dr_s[G], qn_r[G], qn_s[G], atyn_r[G], atyn_s[G], pxn_r[G], pxn_s[G];
+        {
+            T px[G][NS], aty[G][NS];
+            tile_mv_g<T, G, NT, KN, KNP>(img + L.PW, xs, px, lane, nullptr);
+            tile_mv_g<T, G, NT, KM, KMP>(img + L.AhT, y, aty, lane, nullptr);
+            const T *Dinv = fresh_ptr((const T *)s_Dinv);
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                dr_r[gi] = dr_s[gi] = qn_r[gi] = qn_s[gi] = atyn_r[gi] = atyn_s[gi] = pxn_r[gi] = pxn_s[gi] = T(0);
+#pragma unroll
+                for (int s = 0; s < KN; s++) {
+                    const T qhs = qh[gi][s];
+                    const T r = (qhs + px[gi][s]) + aty[gi][s];
+                    const T di = Dinv[4 * s + g];
+                    dr_r[gi] = nrm(dr_r[gi], r);
+                    dr_s[gi] = nrm(dr_s[gi], di * r);
+                    qn_r[gi] = nrm(qn_r[gi], qhs);
+                    qn_s[gi] = nrm(qn_s[gi], di * qhs);
+                    atyn_r[gi] = nrm(atyn_r[gi], aty[gi][s]);
+                    atyn_s[gi] = nrm(atyn_s[gi], di * aty[gi][s]);
+                    pxn_r[gi] = nrm(pxn_r[gi], px[gi][s]);
+                    pxn_s[gi] = nrm(pxn_s[gi], di * px[gi][s]);
+                }
+            }
+        }
+        T pri_res[G], dua_res[G];
+        const T cinv = op.cs[1];
+#pragma unroll
+        for (int gi = 0; gi < G; gi++) {
+            ax_z[gi] = col_max(ax_z[gi]); ax_zs[gi] = col_max(ax_zs[gi]);
+            zn_s[gi] = col_max(zn_s[gi]); zn_r[gi] = col_max(zn_r[gi]);
+            axn_s[gi] = col_max(axn_s[gi]); axn_r[gi] = col_max(axn_r[gi]);
+            dr_r[gi] = col_max(dr_r[gi]); dr_s[gi] = col_max(dr_s[gi]);
+            qn_r[gi] = col_max(qn_r[gi]); qn_s[gi] = col_max(qn_s[gi]);
+            atyn_r[gi] = col_max(atyn_r[gi]); atyn_s[gi] = col_max(atyn_s[gi]);
+            pxn_r[gi] = col_max(pxn_r[gi]); pxn_s[gi] = col_max(pxn_s[gi]);
+            pri_res[gi] = scaled_term ? ax_z[gi] : ax_zs[gi];
+            dua_res[gi] = scaled_term ? dr_r[gi] : cinv * dr_s[gi];
+        }
+
+        // OSQP is_primal_infeasible on delta_y = dy (this iteration's dual step), per group.
+        auto primal_infeasible = [&](T eps, const bool (&need)[G], bool (&res)[G]) {
+            T d[G][MS];
+            T ndy[G], lhs[G];
+            const T *E = fresh_ptr((const T *)s_E);
+            bool cand[G], anyc = false;
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                ndy[gi] = lhs[gi] = T(0);
+#pragma unroll
+                for (int s = 0; s < MS; s++) {
+                    if (s >= KM) { d[gi][s] = T(0); continue; }
+                    T dd = dy[gi][s];
+                    const T up = uh[gi][s], lo = LFREE ? T(-kInfty) : lh[gi][s];
+                    const bool uinf = up > T(kInfty * kMinScaling), linf = lo < T(-kInfty * kMinScaling);
+                    if (uinf) dd = linf ? T(0) : tt_min(dd, T(0));
+                    else if (linf) dd = tt_max(dd, T(0));
+                    d[gi][s] = dd;
+                    ndy[gi] = nrm(ndy[gi], scaled_term ? dd : E[4 * s + g] * dd);
+                    if (up < T(kInfty * kMinScaling)) lhs[gi] += up * tt_max(dd, T(0));
+                    if (lo > T(-kInfty * kMinScaling)) lhs[gi] += lo * tt_min(dd, T(0));
+                }
+                ndy[gi] = col_max(ndy[gi]);
+                lhs[gi] = col_sum(lhs[gi]);
+                cand[gi] = need[gi] && ndy[gi] > T(kDivisionTol) && lhs[gi] < eps * ndy[gi];
+                res[gi] = false;
+                anyc = anyc || cand[gi];
+            }
+            if (!wave_any(anyc)) return;
+            T atd[G][NS];
+            tile_mv_g<T, G, NT, KM, KMP>(img + L.AhT, d, atd, lane, nullptr);
+            const T *Dinv = fresh_ptr((const T *)s_Dinv);
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                T nat = 0;
+#pragma unroll
+                for (int s = 0; s < KN; s++) nat = nrm(nat, scaled_term ? atd[gi][s] : Dinv[4 * s + g] * atd[gi][s]);
+                nat = col_max(nat);
+                res[gi] = cand[gi] && nat < eps * ndy[gi];
+            }
+        };
+        // OSQP is_dual_infeasible on delta_x^ = W dx, per group.
+        auto dual_infeasible = [&](T eps, const bool (&need)[G], bool (&res)[G]) {
+            T qdx[G];
+            bool cand[G], anyc = false;
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                qdx[gi] = T(0);  // q^' dx^ = (W' q^)' dx' = -gv' dx'
+#pragma unroll
+                for (int s = 0; s < KN; s++) qdx[gi] = tt_fma(-gv[gi][s], dx[gi][s], qdx[gi]);
+                qdx[gi] = col_sum(qdx[gi]);
+                cand[gi] = need[gi] && qdx[gi] < T(0);
+                res[gi] = false;
+                anyc = anyc || cand[gi];
+            }
+            if (!wave_any(anyc)) return;
+            T t1[G][NS], ndx[G];
+            tile_mv_g<T, G, NT, KN, KNP>(img + L.W, dx, t1, lane, nullptr);
+            const T *D = fresh_ptr((const T *)s_D);
+            const T cs = scaled_term ? T(1) : op.cs[0];
+            anyc = false;
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                ndx[gi] = T(0);
+#pragma unroll
+                for (int s = 0; s < KN; s++) ndx[gi] = nrm(ndx[gi], scaled_term ? t1[gi][s] : D[4 * s + g] * t1[gi][s]);
+                ndx[gi] = col_max(ndx[gi]);
+                cand[gi] = cand[gi] && ndx[gi] > T(kDivisionTol) && qdx[gi] < -cs * eps * ndx[gi];
+                anyc = anyc || cand[gi];
+            }
+            if (!wave_any(anyc)) return;
+            tile_mv_g<T, G, NT, KN, KNP>(img + L.PW, dx, t1, lane, nullptr);
+            const T *Dinv = fresh_ptr((const T *)s_Dinv);
+            anyc = false;
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                T npdx = 0;
+#pragma unroll
+                for (int s = 0; s < KN; s++) npdx = nrm(npdx, scaled_term ? t1[gi][s] : Dinv[4 * s + g] * t1[gi][s]);
+                npdx = col_max(npdx);
+                cand[gi] = cand[gi] && npdx < cs * eps * ndx[gi];
+                anyc = anyc || cand[gi];
+            }
+            if (!wave_any(anyc)) return;
+            T adx[G][MS];
+            tile_mv_g<T, G, MT, KN, KNP>(img + L.B, dx, adx, lane, nullptr);
+            const T *Einv = fresh_ptr((const T *)s_Einv);
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                int viol = 0;
+#pragma unroll
+                for (int s = 0; s < KM; s++) {
+                    const T sv = scaled_term ? adx[gi][s] : Einv[4 * s + g] * adx[gi][s];
+                    const T up = uh[gi][s], lo = LFREE ? T(-kInfty) : lh[gi][s];
+                    if ((up < T(kInfty * kMinScaling) && sv > eps * ndx[gi]) ||
+                        (lo > T(-kInfty * kMinScaling) && sv < -eps * ndx[gi]))
+                        viol = 1;
+                }
+                viol = col_or(viol);
+                res[gi] = cand[gi] && !viol;
+            }
+        };
+        // check_termination(approximate) — OSQP auxil.c; new status per group (kUnsolved: go on)
+        auto check_termination = [&](bool approx, const bool (&need0)[G], int (&out)[G]) {
+            const T mul = approx ? T(10) : T(1);
+            const T ea = eps_abs * mul, er = eps_rel * mul;
+            bool noncvx[G], prim_ok[G], dual_ok[G], need_p[G], need_d[G], prim_inf[G], dual_inf[G];
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                noncvx[gi] = pri_res[gi] > T(kInfty) || dua_res[gi] > T(kInfty);
+                const bool need = need0[gi] && !noncvx[gi];  // every lane runs the (uniform) code below
+                prim_ok[gi] = (m == 0);
+                need_p[gi] = false;
+                if (m > 0) {
+                    const T ep = ea + er * (scaled_term ? tt_max(zn_r[gi], axn_r[gi]) : tt_max(zn_s[gi], axn_s[gi]));
+                    prim_ok[gi] = pri_res[gi] < ep;
+                    need_p[gi] = need && !prim_ok[gi];
+                }
+                const T ed = ea + er * (scaled_term ? tt_max(tt_max(qn_r[gi], atyn_r[gi]), pxn_r[gi])
+                                                    : cinv * tt_max(tt_max(qn_s[gi], atyn_s[gi]), pxn_s[gi]));
+                dual_ok[gi] = dua_res[gi] < ed;
+                need_d[gi] = need && !dual_ok[gi];
+            }
+            primal_infeasible((T)st.eps_prim_inf * mul, need_p, prim_inf);
+            dual_infeasible((T)st.eps_dual_inf * mul, need_d, dual_inf);
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                int o = kUnsolved;
+                if (noncvx[gi]) o = kNonCvx;
+                else if (prim_ok[gi] && dual_ok[gi]) o = approx ? kSolvedInaccurate : kSolved;
+                else if (prim_inf[gi]) o = approx ? kPrimalInfeasibleInaccurate : kPrimalInfeasible;
+                else if (dual_inf[gi]) o = approx ? kDualInfeasibleInaccurate : kDualInfeasible;
+                out[gi] = o;
+            }
+        };
+
+        bool term[G], need[G];
+#pragma unroll
+        for (int gi = 0; gi < G; gi++) {
+            term[gi] = done[gi];  // finished (or dead) columns ignore everything below
+            need[gi] = !term[gi];
+        }
+        if (at_check) {
+            int s0[G];
+            check_termination(false, need, s0);
+#pragma unroll
+            for (int gi = 0; gi < G; gi++)
+                if (!term[gi] && s0[gi] != kUnsolved) { status[gi] = s0[gi]; term[gi] = true; }
+        }
+        if (at_adapt) {  // adapt_rho / compute_rho_estimate (scaled-space norms)
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                if (term[gi]) continue;
+                const T pr = ax_z[gi] / (tt_max(zn_r[gi], axn_r[gi]) + T(kDivisionTol));
+                const T dn = tt_max(tt_max(qn_r[gi], atyn_r[gi]), pxn_r[gi]);
+                const T du = dr_r[gi] / (dn + T(kDivisionTol));
+                T rn = rho[gi] * (T)sqrt((double)(pr / (du + T(kDivisionTol))));
+                rn = tt_min(tt_max(rn, T(kRhoMin)), T(kRhoMax));
+                if (rn > rho[gi] * (T)st.adaptive_rho_tolerance || rn < rho[gi] / (T)st.adaptive_rho_tolerance) {
+                    rho[gi] = tt_min(tt_max(rn, T(kRhoMin)), T(kRhoMax));
+                    rinv[gi] = T(1) / rho[gi];
+                }
+            }
+            set_dk();  // uniform; unchanged rho gives the same dk bit for bit
+        }
+        if (last) {  // after the ADMM loop (osqp_solve)
+            int s1[G], s2[G];
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                need[gi] = !term[gi];
+                s1[gi] = kUnsolved;
+            }
+            if (!at_check) check_termination(false, need, s1);
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                if (!term[gi] && s1[gi] != kUnsolved) { status[gi] = s1[gi]; term[gi] = true; }
+                need[gi] = !term[gi];
+            }
+            check_termination(true, need, s2);
+#pragma unroll
+            for (int gi = 0; gi < G; gi++)
+                if (!term[gi]) { status[gi] = s2[gi] != kUnsolved ? s2[gi] : kMaxIterReached; term[gi] = true; }
+        }
+        {
+            bool newly[G], any = false;
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                newly[gi] = term[gi] && !done[gi];
+                any = any || newly[gi];
+            }
+            if (wave_any(any)) finalize(newly);
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) done[gi] = term[gi];
+        }
+        if (it == stop && !all_done()) {
+            // phase boundary: save the running QPs and queue them for the next launch
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                const bool run = !done[gi];
+                const int b = opaque(b_[gi]);
+                if (run) {
+#pragma unroll
+                    for (int s = 0; s < NS; s++)
+                        if (s < KN) a.xs[(size_t)b * ncs + 4 * s + g] = xs[gi][s];
+#pragma unroll
+                    for (int s = 0; s < MS; s++)
+                        if (s < KM) {
+                            a.zs[(size_t)b * mcs + 4 * s + g] = z[gi][s];
+                            a.ys[(size_t)b * mcs + 4 * s + g] = y[gi][s];
+                        }
+                    if (g == 0) {
+                        a.rhos[b] = rho[gi];
+                        a.it_state[b] = it;
+                    }
+                }
+                const unsigned long long mask = __ballot(run && g == 0);
+                int base = 0;
+                if (lane == 0 && mask) base = atomicAdd(a.count_out, __popcll(mask));
+                base = __shfl(base, 0);
+                if (run && g == 0) a.list_out[base + __popcll(mask & ((1ull << lane) - 1ull))] = b;
+            }
             break;
         }
     }
 }
 
-// occ: 0 = default for the shape/type, else a requested register budget (3 or 4 waves/SIMD) for
-// the f32 fast variant (benchmark A/B hook).
+// occ: 0 = default for the shape/type, else a requested variant (benchmark A/B hook):
+// f32 fast path  occ 3 -> 1 group/wave at 3 waves/SIMD;  occ 2 -> 2 groups/wave at 2 waves/SIMD.
 template <typename T, int KN, int KM>
 int tile_launch(const AdmmArgs<T> &a, int occ, hipStream_t s)
 {
-    const dim3 grid((a.batch + 63) / 64), block(256);
+    const dim3 block(256);
+    auto grid = [&](int G) { return dim3((a.batch + 64 * G - 1) / (64 * G)); };
     if (a.all_ineq && a.lower_free) {
-        if constexpr (sizeof(T) == 8)
-            hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 2>), grid, block, 0, s, a);
-        else if (occ == 4)
-            hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 4>), grid, block, 0, s, a);
-        else  // default: 3 waves/SIMD — the whole iteration fits in registers (no spills)
-            hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 3>), grid, block, 0, s, a);
+        if constexpr (sizeof(T) == 8) {
+            if (occ == 1)
+                hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 2, 1>), grid(2), block, 0, s, a);
+            else
+                hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 1, 2>), grid(1), block, 0, s, a);
+        } else {
+            if (occ == 2)
+                hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 2, 2>), grid(2), block, 0, s, a);
+            else
+                hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 1, 3>), grid(1), block, 0, s, a);
+        }
     } else {
-        hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, false, false, 2>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, false, false, 1, 2>), grid(1), block, 0, s, a);
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
