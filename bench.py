@@ -39,7 +39,15 @@ def parse():
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=0)
-    return p.parse_args()
+    p.add_argument("--workload", choices=("cfg2", "stream"), default="cfg2",
+                   help="cfg2: BASELINE config 2 (the headline); stream: config 5 (4,096 plants x --ctrl-steps "
+                        "warm-started control steps with a simulated plant, hipGraph-replayed)")
+    p.add_argument("--ctrl-steps", type=int, default=1000, help="control steps per bench step (stream)")
+    p.add_argument("--noise", type=float, default=1e-2, help="plant noise std (stream; SURVEY §8d: var 1e-4)")
+    a = p.parse_args()
+    if a.workload == "stream" and a.batch == 65536:
+        a.batch = 4096
+    return a
 
 
 def cpu_baseline(ops, N, X, U, budget_s, threads):
@@ -117,27 +125,54 @@ def main():
     sptr = stream.cuda_stream
     gathered = [torch.empty_like(U_d) for _ in range(world)] if rank == 0 else None
 
-    def step():
+    stream_mode = a.workload == "stream"
+    if stream_mode:
+        solver.mpc_set_plant(plant["Ad"], plant["Bd"])
+        side = torch.cuda.Stream(dev)  # graph capture needs a non-default stream
+        stream, sptr = side, side.cuda_stream
+        X0_d = X_d.clone()
+    ctrl_base = [0]
+
+    def launch():
+        if stream_mode:  # config 5: ctrl_steps warm-started control steps + plant updates (hipGraph)
+            solver.mpc_run_device(X_d.data_ptr(), U_d.data_ptr(), plant["xref"], a.ctrl_steps, a.seed, start,
+                                  ctrl_base[0], a.noise, sptr)
+            ctrl_base[0] += a.ctrl_steps
+        else:
+            solver.mpc_step_device(X_d.data_ptr(), U_d.data_ptr(), plant["xref"], sptr)
+
+    def reset():
         U_d.copy_(U0_d)          # every step: the reference's first control step of each plant
         solver.reset_state()     # post-setup solver state (x = z = y = 0, rho = settings.rho)
-        solver.mpc_step_device(X_d.data_ptr(), U_d.data_ptr(), plant["xref"], sptr)
+        if stream_mode:
+            X_d.copy_(X0_d)
+            ctrl_base[0] = 0
+
+    cur = torch.cuda.current_stream(dev)
+
+    def step(i=None):
+        reset()
+        if stream_mode:
+            stream.wait_stream(cur)  # the resets above ran on the current stream
+        if i is not None:
+            ev[i][0].record(stream)
+        launch()
+        if i is not None:
+            ev[i][1].record(stream)
+        if stream_mode:
+            cur.wait_stream(stream)
         mdist.gather_moves(dist, U_d, world, rank, gathered)
 
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
     t0 = time.perf_counter()
     for i in range(a.steps):
-        U_d.copy_(U0_d)
-        solver.reset_state()
-        ev[i][0].record(stream)
-        solver.mpc_step_device(X_d.data_ptr(), U_d.data_ptr(), plant["xref"], sptr)
-        ev[i][1].record(stream)
-        mdist.gather_moves(dist, U_d, world, rank, gathered)
+        step(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -150,7 +185,9 @@ def main():
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
 
     status, iters, _ = solver.info()
-    flops = float(workload.flops_per_qp(N, 2 * N, 4, iters).sum())
+    qps_per_step = B * (a.ctrl_steps if stream_mode else 1)
+    # stream: iterations of the last control step stand for every step (estimate, see "flops_note")
+    flops = float(workload.flops_per_qp(N, 2 * N, 4, iters).sum()) * (a.ctrl_steps if stream_mode else 1)
     achieved = flops / (kern_ms * 1e-3) / 1e12
     solved = float(np.mean(status == sm.SOLVED))
 
@@ -158,7 +195,7 @@ def main():
         if dist:
             dist.destroy_process_group()
         return
-    total_qps = B * world * a.steps / wall
+    total_qps = qps_per_step * world * a.steps / wall
     rec = {
         "metric": "QP solves/sec (n_x=4, n_u=1, N=20 batch)",
         "value": total_qps,
@@ -172,18 +209,22 @@ def main():
         "vs_baseline": None,
         "dtype": a.dtype,
         "data": "synthetic (counter-based X ~ N(0, diag(.1,.1,.05,.5)), U ~ U(-1,1); reference plant config)",
-        "config": {"workload": f"cfg2: {B} identical LTI plants per GPU, N={N} (n={N}, m={2 * N}), "
-                               f"one controllerStep each", "batch_per_gpu": B, "horizon": N,
-                   "parallelism": f"dp{world}"},
+        "config": ({"workload": f"cfg2: {B} identical LTI plants per GPU, N={N} (n={N}, m={2 * N}), "
+                                f"one controllerStep each", "batch_per_gpu": B, "horizon": N,
+                    "parallelism": f"dp{world}"} if not stream_mode else
+                   {"workload": f"cfg5: {B} plants per GPU x {a.ctrl_steps} warm-started control steps, "
+                                f"simulated plant (noise std {a.noise}), hipGraph-replayed, N={N}",
+                    "batch_per_gpu": B, "horizon": N, "ctrl_steps": a.ctrl_steps, "parallelism": f"dp{world}"}),
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS[a.dtype], "unit": "TFLOP/s",
                      "frac": achieved / PEAK_TFLOPS[a.dtype], "traffic": traffic_per_solve(a.dtype, B, N),
                      "kernel": "admm_tile_kernel (all phase launches of one solve)",
                      "kernel_ms": kern_ms, "flops_per_solve": flops,
                      "flops_note": "algorithmic: sum over QPs of iters*F_iter + checks*F_check + front end "
-                                   "(SURVEY §8d, DESIGN §4.1), actual per-QP iteration counts"},
+                                   "(SURVEY §8d, DESIGN §4.1), actual per-QP iteration counts"
+                                   + ("; stream: last control step's counts x ctrl_steps (estimate)" if stream_mode else "")},
         "iters": {"mean": float(iters.mean()), "max": int(iters.max()), "solved_frac": solved},
     }
-    if a.cpu_seconds > 0:
+    if a.cpu_seconds > 0 and not stream_mode:
         rec["cpu_baseline"] = cpu_baseline(ops, N, X, U, a.cpu_seconds, a.cpu_threads)
     print(json.dumps(rec))
     if dist:

@@ -147,6 +147,22 @@ int mpcq_mpc_step_device(mpcq_ctx *ctx, const double *X_dev, double *U_dev, doub
 /* Host-memory convenience form of mpcq_mpc_step_device (copies in/out, synchronises). */
 int mpcq_mpc_step(mpcq_ctx *ctx, const double *X, double *U, double xref);
 
+/* ---- receding-horizon stream (BASELINE config 5; the solver.cpp loop, solver.cpp:43-74, with the
+ * serial plant replaced by a simulated one) ----------------------------------------------------
+ * Plant of every QP: X <- Ad X + Bd U + w,  w ~ N(0, noise_std^2 I) drawn from a counter-based
+ * generator keyed by (seed, global QP index first_qp + b, step, component) — the same stream on any
+ * sharding of the batch (solvempc_amd/workload.py restates it).  Ad nx*nx, Bd nx per plant. */
+int mpcq_mpc_set_plant(mpcq_ctx *ctx, int nx, const double *Ad, const double *Bd);
+/* One plant update on device-resident X (batch*nx) / U (batch); `step` selects the noise draw. */
+int mpcq_mpc_simulate_device(mpcq_ctx *ctx, double *X_dev, const double *U_dev, unsigned long long seed,
+                             long long first_qp, long long step, double noise_std, void *stream);
+/* `steps` warm-started control steps  [controllerStep (:81-108) ; plant update]  for every QP,
+ * captured once as a hipGraph and replayed (steps first_step .. first_step+steps-1).  X_dev/U_dev
+ * evolve in place.  `stream` must not be the NULL stream (graph capture). */
+int mpcq_mpc_run_device(mpcq_ctx *ctx, double *X_dev, double *U_dev, double xref, int steps,
+                        unsigned long long seed, long long first_qp, long long first_step,
+                        double noise_std, void *stream);
+
 /* Condensed-QP construction on device `device` for n_plants SISO plants (ModelPredictiveControlAPI
  * setTransformations / setLL / setLiftedCosts / setH / setFVars / setLinearConstraints /
  * setUpperBound, src/ModelPredictiveControlAPI.cpp:158-369).  Inputs per plant: Ad nx*nx, Bd nx,

@@ -65,8 +65,11 @@ class BatchSolver:
     def close(self):
         ctx = getattr(self, "_ctx", None)
         if ctx:
-            lib().mpcq_destroy(ctx)
             self._ctx = None
+            try:
+                lib().mpcq_destroy(ctx)
+            except TypeError:  # interpreter shutdown: module globals already torn down
+                pass
 
     def __del__(self):
         self.close()
@@ -167,6 +170,27 @@ class BatchSolver:
         U = _c64(U).reshape(self.batch).copy()
         _capi.check(lib().mpcq_mpc_step(self._ctx, _dp(X), _dp(U), float(xref)), "mpcq_mpc_step")
         return U
+
+    # -- receding-horizon stream (BASELINE config 5): simulated plant + graph-captured control steps
+    def mpc_set_plant(self, Ad, Bd) -> None:
+        k = self.n_plants
+        Ad = _c64(Ad).reshape(k, -1)
+        nx = int(round(np.sqrt(Ad.shape[1])))
+        Bd = _c64(Bd).reshape(k, nx)
+        _capi.check(lib().mpcq_mpc_set_plant(self._ctx, nx, _dp(Ad), _dp(Bd)), "mpcq_mpc_set_plant")
+
+    def mpc_simulate_device(self, X_ptr: int, U_ptr: int, seed: int, first_qp: int, step: int,
+                            noise_std: float, stream: int | None = None) -> None:
+        _capi.check(lib().mpcq_mpc_simulate_device(self._ctx, C.c_void_p(X_ptr), C.c_void_p(U_ptr), seed, first_qp,
+                                                   step, float(noise_std), C.c_void_p(stream or 0)),
+                    "mpcq_mpc_simulate_device")
+
+    def mpc_run_device(self, X_ptr: int, U_ptr: int, xref: float, steps: int, seed: int, first_qp: int,
+                       first_step: int, noise_std: float, stream: int) -> None:
+        """``steps`` warm-started [controllerStep; plant update] rounds, replayed from a hipGraph."""
+        _capi.check(lib().mpcq_mpc_run_device(self._ctx, C.c_void_p(X_ptr), C.c_void_p(U_ptr), float(xref),
+                                              int(steps), seed, first_qp, first_step, float(noise_std),
+                                              C.c_void_p(stream)), "mpcq_mpc_run_device")
 
     def mpc_step_device(self, X_ptr: int, U_ptr: int, xref: float = 0.0, stream: int | None = None) -> None:
         """Same on device-resident fp64 buffers (e.g. torch tensors' data_ptr()); asynchronous."""

@@ -17,7 +17,8 @@ EXPORTS = (
     "mpcq_update_upper_bound", "mpcq_update_lower_bound", "mpcq_update_bounds", "mpcq_warm_start",
     "mpcq_cold_start", "mpcq_reset", "mpcq_solve", "mpcq_get_solution", "mpcq_get_dual", "mpcq_get_info",
     "mpcq_get_scaling", "mpcq_device_view_get", "mpcq_mpc_set_operators", "mpcq_mpc_step_device",
-    "mpcq_mpc_step", "mpcq_condense", "mpcq_last_error",
+    "mpcq_mpc_step", "mpcq_mpc_set_plant", "mpcq_mpc_simulate_device", "mpcq_mpc_run_device",
+    "mpcq_condense", "mpcq_last_error",
 )
 
 
@@ -87,6 +88,10 @@ def lib() -> C.CDLL:
         "mpcq_mpc_set_operators": (C.c_int, [vp, C.c_int, dp, dp, dp, dp, dp, dp]),
         "mpcq_mpc_step_device": (C.c_int, [vp, vp, vp, C.c_double, vp]),
         "mpcq_mpc_step": (C.c_int, [vp, dp, dp, C.c_double]),
+        "mpcq_mpc_set_plant": (C.c_int, [vp, C.c_int, dp, dp]),
+        "mpcq_mpc_simulate_device": (C.c_int, [vp, vp, vp, C.c_ulonglong, C.c_longlong, C.c_longlong, C.c_double, vp]),
+        "mpcq_mpc_run_device": (C.c_int, [vp, vp, vp, C.c_double, C.c_int, C.c_ulonglong, C.c_longlong,
+                                          C.c_longlong, C.c_double, vp]),
         "mpcq_condense": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int] + [dp] * 15),
         "mpcq_last_error": (C.c_char_p, []),
     }

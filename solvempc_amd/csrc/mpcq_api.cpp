@@ -66,6 +66,13 @@ struct mpcq_ctx {
     // MPC front end
     double *d_Fx = nullptr, *d_Fu = nullptr, *d_Fr = nullptr, *d_Sbar = nullptr, *d_Ku = nullptr, *d_W0 = nullptr;
     double *d_X = nullptr, *d_U = nullptr;
+    // receding-horizon stream: plant, step counter, captured graph of one control step
+    double *d_Ad = nullptr, *d_Bd = nullptr;
+    long long *d_step = nullptr;
+    int plant_nx = 0;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t gexec = nullptr;
+    struct { double *X, *U; double xref, noise; unsigned long long seed; long long first_qp; hipStream_t s; } gkey{};
     // host copies of plant-0 scaling
     std::vector<double> hD, hE;
     double hc = 1.0;
@@ -338,7 +345,9 @@ int mpcq_destroy(mpcq_ctx *c)
                     c->d_setup_status, c->d_q, c->d_u, c->d_l, c->d_x, c->d_y, c->d_rho, c->d_status, c->d_iter,
                     c->d_xs, c->d_zs, c->d_ys, c->d_rhos, c->d_snx, c->d_sny, c->d_Fx, c->d_Fu, c->d_Fr,
                     c->d_Sbar, c->d_Ku, c->d_W0, c->d_X, c->d_U, c->d_img, c->d_list, c->d_counts,
-                    c->d_itstate};
+                    c->d_itstate, c->d_Ad, c->d_Bd, c->d_step};
+    if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
+    if (c->graph) (void)hipGraphDestroy(c->graph);
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete c;
@@ -541,7 +550,9 @@ static int launch_args(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s)
     // phases whose QPs are few (the slow tail) run one QP per wave
     const char *te = std::getenv("MPCQ_TAIL_PHASE");
     const bool all_wave = std::strcmp(env_kernel(), "wave") == 0;
-    const int tail_from = all_wave ? 0 : (te ? std::atoi(te) : 3);
+    // Small batches (under 512 tile waves) are latency-bound: one QP per wave from the start.
+    const bool small = B < 8192 && std::strcmp(env_kernel(), "tile") != 0;
+    const int tail_from = (all_wave || small) ? 0 : (te ? std::atoi(te) : 3);
 
     for (int p = 0; p < np; p++) {
         a.img = (const T *)c->d_img;
@@ -714,6 +725,97 @@ int mpcq_mpc_step(mpcq_ctx *c, const double *X, double *U, double xref)
     if ((rc = h2d(c->d_X, X, 8 * B * c->nx, c->last)) || (rc = h2d(c->d_U, U, 8 * B, c->last))) return rc;
     if ((rc = launch_solve(c, c->last, true, c->d_X, c->d_U, xref))) return rc;
     return d2h(c, U, c->d_U, 8 * B);
+}
+
+int mpcq_mpc_set_plant(mpcq_ctx *c, int nx, const double *Ad, const double *Bd)
+{
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    if (nx <= 0 || nx > 8 || !Ad || !Bd) return fail(MPCQ_ERR_ARG, "set_plant: 1 <= nx <= 8 and Ad, Bd required");
+    const size_t Pn = c->dims.n_plants;
+    if (c->plant_nx != nx) {
+        for (double **p : {&c->d_Ad, &c->d_Bd})
+            if (*p) { (void)hipFree(*p); *p = nullptr; }
+    }
+    if ((!c->d_Ad && hipMalloc((void **)&c->d_Ad, 8 * Pn * nx * nx) != hipSuccess) ||
+        (!c->d_Bd && hipMalloc((void **)&c->d_Bd, 8 * Pn * nx) != hipSuccess) ||
+        (!c->d_step && hipMalloc((void **)&c->d_step, 8) != hipSuccess))
+        return fail(MPCQ_ERR_HIP, "hipMalloc failed");
+    c->plant_nx = nx;
+    if ((rc = h2d(c->d_Ad, Ad, 8 * Pn * nx * nx, c->last)) || (rc = h2d(c->d_Bd, Bd, 8 * Pn * nx, c->last))) return rc;
+    return MPCQ_OK;
+}
+
+int mpcq_mpc_simulate_device(mpcq_ctx *c, double *X, const double *U, unsigned long long seed, long long first_qp,
+                             long long step, double noise_std, void *stream)
+{
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    if (!c->plant_nx) return fail(MPCQ_ERR_ORDER, "mpcq_mpc_set_plant has not been called");
+    if (!X || !U) return fail(MPCQ_ERR_ARG, "null X/U");
+    if (mpcq_internal_simulate(c->dims.batch, c->plant_nx, c->dims.n_plants == 1, c->d_Ad, c->d_Bd, X, U, seed,
+                               first_qp, nullptr, step, noise_std, (hipStream_t)stream))
+        return fail(MPCQ_ERR_HIP, "simulate kernel launch failed");
+    c->last = (hipStream_t)stream;
+    return MPCQ_OK;
+}
+
+int mpcq_mpc_run_device(mpcq_ctx *c, double *X, double *U, double xref, int steps, unsigned long long seed,
+                        long long first_qp, long long first_step, double noise_std, void *stream)
+{
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (!c->mpc_ready || !c->plant_nx) return fail(MPCQ_ERR_ORDER, "mpc operators / plant not set");
+    if (c->plant_nx != c->nx) return fail(MPCQ_ERR_ARG, "plant nx differs from the operators' nx");
+    if (!X || !U || steps < 0) return fail(MPCQ_ERR_ARG, "null X/U or steps < 0");
+    if (!stream) return fail(MPCQ_ERR_ARG, "graph capture needs a non-NULL stream");
+    hipStream_t s = (hipStream_t)stream;
+    if (steps == 0) return MPCQ_OK;
+    if (mpcq_internal_set_step(c->d_step, first_step, s)) return fail(MPCQ_ERR_HIP, "set_step launch failed");
+    const char *dbg = std::getenv("MPCQ_DEBUG_SYNC");  // debugging hook: synchronise every stage
+    const bool sync_each = dbg && dbg[0] == '1';
+    auto stage = [&](const char *what) -> int {
+        if (!sync_each) return MPCQ_OK;
+        const hipError_t e = hipStreamSynchronize(s);
+        return e == hipSuccess ? MPCQ_OK : fail(MPCQ_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    };
+    if ((rc = stage("set_step"))) return rc;
+    int done = 0;
+    if (c->fresh) {  // a reset is a one-off (x = z = y = 0): run that step eagerly, capture the rest
+        if ((rc = launch_solve(c, s, true, X, U, xref))) return rc;
+        if (mpcq_internal_simulate(c->dims.batch, c->nx, c->dims.n_plants == 1, c->d_Ad, c->d_Bd, X, U, seed,
+                                   first_qp, c->d_step, 0, noise_std, s) ||
+            mpcq_internal_tick(c->d_step, s))
+            return fail(MPCQ_ERR_HIP, "simulate kernel launch failed");
+        done = 1;
+        if ((rc = stage("eager first step"))) return rc;
+    }
+    const bool same = c->gexec && c->gkey.X == X && c->gkey.U == U && c->gkey.xref == xref &&
+                      c->gkey.noise == noise_std && c->gkey.seed == seed && c->gkey.first_qp == first_qp &&
+                      c->gkey.s == s;
+    if (!same && done < steps) {
+        if (c->gexec) { (void)hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+        if (c->graph) { (void)hipGraphDestroy(c->graph); c->graph = nullptr; }
+        HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        int lrc = launch_solve(c, s, true, X, U, xref);
+        if (!lrc && (mpcq_internal_simulate(c->dims.batch, c->nx, c->dims.n_plants == 1, c->d_Ad, c->d_Bd, X, U,
+                                            seed, first_qp, c->d_step, 0, noise_std, s) ||
+                     mpcq_internal_tick(c->d_step, s)))
+            lrc = fail(MPCQ_ERR_HIP, "simulate kernel launch failed");
+        hipGraph_t g = nullptr;
+        const hipError_t ec = hipStreamEndCapture(s, &g);
+        if (lrc) { if (g) (void)hipGraphDestroy(g); return lrc; }
+        if (ec != hipSuccess) return fail(MPCQ_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ec));
+        c->graph = g;
+        HIPCHK(hipGraphInstantiate(&c->gexec, c->graph, nullptr, nullptr, 0));
+        c->gkey = {X, U, xref, noise_std, seed, first_qp, s};
+    }
+    for (int k = done; k < steps; k++) {
+        HIPCHK(hipGraphLaunch(c->gexec, s));
+        if (sync_each && (rc = stage(("graph replay " + std::to_string(k)).c_str()))) return rc;
+    }
+    c->last = s;
+    return MPCQ_OK;
 }
 
 int mpcq_condense(int device, int n_plants, int nx, int N, int s_rows, const double *Ad, const double *Bd,

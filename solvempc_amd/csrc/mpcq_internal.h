@@ -214,6 +214,12 @@ int mpcq_internal_tile_launch_f32(const mpcq::AdmmArgs<float> *a, int KN, int KM
 // -1 = n > 32 or m > 64 (not compiled).
 int mpcq_internal_wave_launch_f64(const mpcq::AdmmArgs<double> *a, int nc, int mc, int grid, hipStream_t s);
 int mpcq_internal_wave_launch_f32(const mpcq::AdmmArgs<float> *a, int nc, int mc, int grid, hipStream_t s);
+// Plant update of the receding-horizon stream (mpcq_stream.hip); step from *step_p when non-null.
+int mpcq_internal_simulate(int batch, int nx, int shared, const double *Ad, const double *Bd, double *X,
+                           const double *U, unsigned long long seed, long long first_qp, const long long *step_p,
+                           long long step_v, double noise_std, hipStream_t s);
+int mpcq_internal_tick(long long *step, hipStream_t s);
+int mpcq_internal_set_step(long long *step, long long v, hipStream_t s);
 // Build the TileLayout images (type T = f32 if is_f32) of plant 0 from its fp64 operator block.
 int mpcq_internal_tile_images(const double *ops, int nc, int mc, int KN, int KM, int is_f32, void *img,
                               hipStream_t s);

@@ -442,7 +442,7 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
 }
 
 template <typename T, int NCAP, int MCAP, bool ALL_INEQ, bool LFREE>
-__global__ __launch_bounds__(64) void admm_wave_kernel(AdmmArgs<T> a, int nc, int mc)
+__global__ __launch_bounds__(64, 2) void admm_wave_kernel(AdmmArgs<T> a, int nc, int mc)
 {
     static_assert(NCAP <= 64 && MCAP <= 64, "one row per lane");
     constexpr int VEC = 16 / sizeof(T);

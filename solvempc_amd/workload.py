@@ -21,10 +21,11 @@ def _splitmix64(x: np.ndarray) -> np.ndarray:
         return z ^ (z >> np.uint64(31))
 
 
-def uniforms(seed: int, start: int, count: int, draws: int) -> np.ndarray:
-    """(count, draws) uniforms in (0, 1) for global QP indices start .. start+count-1."""
+def uniforms(seed: int, start: int, count: int, draws: int, draw0: int = 0) -> np.ndarray:
+    """(count, draws) uniforms in (0, 1) for global QP indices start .. start+count-1 (draw indices
+    draw0 .. draw0+draws-1; mpcq_stream.hip's device generator is the same function)."""
     idx = np.arange(start, start + count, dtype=np.uint64)[:, None]
-    d = np.arange(draws, dtype=np.uint64)[None, :]
+    d = np.arange(draw0, draw0 + draws, dtype=np.uint64)[None, :]
     with np.errstate(over="ignore"):
         key = _splitmix64(np.uint64(seed) * np.uint64(0x632BE59BD9B4E019) + np.uint64(1))
         x = _splitmix64(key ^ (idx * np.uint64(0x100000001B3) + d * np.uint64(0xD6E8FEB86659FD93)))
@@ -37,6 +38,23 @@ def normals(seed: int, start: int, count: int, k: int) -> np.ndarray:
     th = 2.0 * np.pi * u[:, 1::2]
     z = np.concatenate([r * np.cos(th), r * np.sin(th)], axis=1)
     return z[:, :k]
+
+
+def plant_noise(seed: int, start: int, count: int, step: int, nx: int, std: float) -> np.ndarray:
+    """w of the simulated plant at control step `step` (mpcq_stream.hip simulate_kernel): Box-Muller
+    pairs from draws step*64 + 2p, 2p+1; component t = r_t cos(th_t) for t < ceil(nx/2), else the sine
+    of pair t - ceil(nx/2)."""
+    npairs = (nx + 1) // 2
+    u = uniforms(seed, start, count, 2 * npairs, draw0=64 * step)
+    r = np.sqrt(-2.0 * np.log(u[:, 0::2]))
+    th = 2.0 * np.pi * u[:, 1::2]
+    z = np.concatenate([r * np.cos(th), r * np.sin(th)], axis=1)[:, :nx]
+    return std * z
+
+
+def simulate(Ad, Bd, X, U, w) -> np.ndarray:
+    """X <- Ad X + Bd U + w for a batch (shared plant)."""
+    return X @ np.asarray(Ad).T + np.asarray(U)[:, None] * np.asarray(Bd)[None, :] + w
 
 
 def mpc_states(seed: int, start: int, count: int, u_range: float = 1.0):

@@ -3,6 +3,10 @@ from pathlib import Path
 
 import pytest
 
+# torch (used by a few GPU tests for device buffers) ships its own HIP runtime; loading it before
+# libmpcq.so makes both share one runtime (the dynamic linker reuses the loaded libamdhip64 SONAME).
+import torch  # noqa: F401,E402
+
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 

@@ -317,3 +317,56 @@ def test_tile_and_wave_paths_agree(plant):
         assert np.array_equal(res["tile"][2], res["wave"][2])  # iterations
         assert np.array_equal(res["tile"][1], res["wave"][1])  # status
         assert np.abs(res["tile"][0] - res["wave"][0]).max() <= tol
+
+
+def test_plant_simulation_matches_host(plant):
+    """mpcq_mpc_simulate_device: X <- Ad X + Bd U + w with the counter-based noise of workload.py."""
+    import torch
+    B, nx = 300, 4
+    X, U = workload.mpc_states(31, 1000, B)
+    s = sm.BatchSolver(20, 40, B)
+    s.mpc_set_plant(plant["Ad"], plant["Bd"])
+    Xd = torch.from_numpy(X.copy()).cuda()
+    Ud = torch.from_numpy(U.copy()).cuda()
+    Xh = X.copy()
+    for step in (0, 1, 7):
+        s.mpc_simulate_device(Xd.data_ptr(), Ud.data_ptr(), 5, 1000, step, 1e-2, 0)
+        torch.cuda.synchronize()
+        Xh = workload.simulate(plant["Ad"], plant["Bd"], Xh, U, workload.plant_noise(5, 1000, B, step, nx, 1e-2))
+        np.testing.assert_allclose(Xd.cpu().numpy(), Xh, rtol=1e-13, atol=1e-15)
+
+
+def test_receding_horizon_stream(plant, kernel):
+    """BASELINE config 5 semantics: warm-started controllerStep (:81-108) + plant update, replayed from a
+    hipGraph one step per call; every step's U matches the oracle driven by the device's X."""
+    import torch
+    N, B, steps = 20, 48, 12
+    ops = oracle.condense(plant, N)
+    l = np.full(2 * N, LMIN)
+    u0 = oracle.upper_bound(ops, np.zeros(4), 0.0)
+    X, U = workload.mpc_states(41, 0, B)
+    s = sm.BatchSolver(N, 2 * N, B)
+    s.setup(ops["P"], np.zeros(N), ops["A"], l, u0)
+    s.mpc_set_operators(ops["Fx"], ops["Fu"], ops["Fr"], ops["Sbar"], ops["Ku"], ops["W0"])
+    s.mpc_set_plant(plant["Ad"], plant["Bd"])
+    Xd = torch.from_numpy(X.copy()).cuda()
+    Ud = torch.from_numpy(U.copy()).cuda()
+    st = torch.cuda.Stream()
+    refs = [oracle.Solver(ops["P"], np.zeros(N), ops["A"], l, u0) for _ in range(B)]
+    Xk, Uk = X.copy(), U.copy()
+    for k in range(steps):
+        with torch.cuda.stream(st):
+            s.mpc_run_device(Xd.data_ptr(), Ud.data_ptr(), 0.0, 1, 9, 0, k, 1e-2, st.cuda_stream)
+        st.synchronize()
+        for b, r in enumerate(refs):
+            assert r.update_gradient(oracle.gradient(ops, Xk[b], Uk[b]))
+            assert r.update_upper_bound(oracle.upper_bound(ops, Xk[b], Uk[b]))
+            if r.solve() == oracle.SOLVED:
+                Uk[b] += r.x()[0]
+        Ug, Xg = Ud.cpu().numpy(), Xd.cpu().numpy()
+        np.testing.assert_allclose(Ug, Uk, rtol=0, atol=1e-9)
+        Xk = workload.simulate(plant["Ad"], plant["Bd"], Xk, Uk, workload.plant_noise(9, 0, B, k, 4, 1e-2))
+        np.testing.assert_allclose(Xg, Xk, rtol=1e-11, atol=1e-12)
+        Xk = Xg.copy()  # keep the oracle on the device's trajectory (libm vs device math: last-ulp noise)
+    _, it, _ = s.info()
+    assert np.median(it) <= 50  # warm start (:52): later steps converge at the first checks
