@@ -302,7 +302,6 @@ int mpcq_create(const mpcq_dims *d, const mpcq_settings *s, mpcq_ctx **out)
     A((void **)&c->d_u0, 8 * P * m);
     A((void **)&c->d_ops, 8 * P * L.total);
     if (d->dtype == MPCQ_F32) A((void **)&c->d_ops32, 4 * P * L.total);
-    A((void **)&c->d_scratch, 8 * P * setup_scratch_len((int)n, (int)m));
     A((void **)&c->d_ctype, 4 * P * mc);
     A((void **)&c->d_setup_status, 4 * P);
     A((void **)&c->d_q, 8 * B * n);
@@ -386,9 +385,19 @@ int mpcq_setup(mpcq_ctx *c, const double *P, const double *q0, const double *A, 
     a.u0 = c->d_u0;
     a.ops = c->d_ops;
     a.ctype = c->d_ctype;
-    a.scratch = c->d_scratch;
     a.status = c->d_setup_status;
-    if (mpcq_internal_setup_launch(&a, s) != 0) return fail(MPCQ_ERR_HIP, "setup kernel launch failed");
+    // one wavefront per plant, LDS-resident (mpcq_setup_wave.hip) where the plant fits; the
+    // global-scratch workgroup kernel otherwise (MPCQ_SETUP=ref forces it: A/B test hook)
+    const char *se = std::getenv("MPCQ_SETUP");
+    const bool ref_setup = (se && !std::strcmp(se, "ref")) || !mpcq_internal_setup_wave_lds((int)n, (int)m);
+    if (ref_setup) {
+        if (!c->d_scratch && hipMalloc((void **)&c->d_scratch, 8 * Pn * setup_scratch_len((int)n, (int)m)) != hipSuccess)
+            return fail(MPCQ_ERR_HIP, "hipMalloc failed (setup scratch)");
+        a.scratch = c->d_scratch;
+        if (mpcq_internal_setup_launch(&a, s) != 0) return fail(MPCQ_ERR_HIP, "setup kernel launch failed");
+    } else if (mpcq_internal_setup_wave_launch(&a, s) != 0) {
+        return fail(MPCQ_ERR_HIP, "setup kernel launch failed");
+    }
     std::vector<int> st(Pn), ct(Pn * c->mc);
     HIPCHK(hipMemcpyAsync(st.data(), c->d_setup_status, 4 * Pn, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(ct.data(), c->d_ctype, 4 * Pn * c->mc, hipMemcpyDeviceToHost, s));

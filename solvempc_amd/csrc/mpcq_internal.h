@@ -194,6 +194,8 @@ struct CondenseArgs {
 // Launchers (extern "C" so the host library links them without templates).
 extern "C" {
 int mpcq_internal_setup_launch(const mpcq::SetupArgs *args, hipStream_t stream);
+int mpcq_internal_setup_wave_launch(const mpcq::SetupArgs *args, hipStream_t stream);
+size_t mpcq_internal_setup_wave_lds(int n, int m);
 int mpcq_internal_f64_to_f32(const double *in, float *out, size_t count, hipStream_t s);
 int mpcq_internal_broadcast(const double *src, double *dst, int len, int batch, int per_qp_src, hipStream_t s);
 int mpcq_internal_fill(void *p, int is_f32, double v, size_t count, hipStream_t s);

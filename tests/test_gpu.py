@@ -370,3 +370,44 @@ def test_receding_horizon_stream(plant, kernel):
         Xk = Xg.copy()  # keep the oracle on the device's trajectory (libm vs device math: last-ulp noise)
     _, it, _ = s.info()
     assert np.median(it) <= 50  # warm start (:52): later steps converge at the first checks
+
+
+@pytest.mark.parametrize("n,m", [(5, 7), (13, 30), (20, 40), (32, 64)])
+def test_setup_wave_vs_workgroup_kernel(n, m):
+    """Per-plant setup, one wave per plant with the parallel-ordering Jacobi (mpcq_setup_wave.hip),
+    against the serial workgroup kernel (MPCQ_SETUP=ref) and the oracle: identical Ruiz scaling, the
+    oracle's status / iteration count and |dx| <= 1e-8 on random convex QPs of odd and even order
+    (equality rows, finite and free lower bounds)."""
+    rng = np.random.default_rng(n * 100 + m)
+    B = 24
+    Ps, As, ls, us, qs = [], [], [], [], []
+    for _ in range(B):
+        M = rng.normal(size=(n, n))
+        Ps.append(M @ M.T + 0.1 * np.eye(n))
+        As.append(rng.normal(size=(m, n)))
+        lo = -rng.uniform(0.5, 2.0, size=m)
+        lo[::5] = -1e30
+        up = rng.uniform(0.5, 2.0, size=m)
+        lo[1] = up[1] = 0.3
+        ls.append(lo); us.append(up); qs.append(rng.normal(size=n))
+    P, A, l, u, q = map(np.stack, (Ps, As, ls, us, qs))
+    out = {}
+    for mode in ("ref", "wave"):
+        os.environ["MPCQ_SETUP"] = mode
+        try:
+            s = sm.BatchSolver(n, m, B, n_plants=B)
+            s.setup(P, np.zeros((B, n)), A, l, u)
+        finally:
+            os.environ.pop("MPCQ_SETUP", None)
+        s.update_lin_cost(q)
+        s.solve()
+        out[mode] = (s.solution(), *s.info(), s.scaling())
+    xr, str_, itr, _, scr = out["ref"]
+    xw, stw, itw, _, scw = out["wave"]
+    for a_, b_ in zip(scr, scw):
+        assert np.array_equal(np.asarray(a_), np.asarray(b_))
+    for b in range(B):
+        x_o, st_o, it_o, _ = oracle.batch_solve(P[b], A[b], np.zeros(n), l[b], u[b], q[b][None], u[b][None])
+        assert stw[b] == st_o[0] and itw[b] == it_o[0], b
+        assert np.abs(xw[b] - x_o[0]).max() < 1e-8
+    assert np.array_equal(stw, str_) and np.abs(xw - xr).max() < 1e-8
