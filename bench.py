@@ -39,14 +39,19 @@ def parse():
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=0)
-    p.add_argument("--workload", choices=("cfg2", "stream"), default="cfg2",
+    p.add_argument("--workload", choices=("cfg2", "stream", "perplant"), default="cfg2",
                    help="cfg2: BASELINE config 2 (the headline); stream: config 5 (4,096 plants x --ctrl-steps "
-                        "warm-started control steps with a simulated plant, hipGraph-replayed)")
+                        "warm-started control steps with a simulated plant, hipGraph-replayed); perplant: config 3 "
+                        "(randomised plants, per-GPU shard of 1M: condense + setup + one controllerStep each)")
     p.add_argument("--ctrl-steps", type=int, default=1000, help="control steps per bench step (stream)")
     p.add_argument("--noise", type=float, default=1e-2, help="plant noise std (stream; SURVEY §8d: var 1e-4)")
     a = p.parse_args()
     if a.workload == "stream" and a.batch == 65536:
         a.batch = 4096
+    if a.workload == "perplant" and a.batch == 65536:
+        a.batch = 131072  # 1,048,576 / 8 GPUs
+        if a.seed == 1:
+            a.seed = 2  # SURVEY §8d config 3 seed
     return a
 
 
@@ -69,6 +74,25 @@ def cpu_baseline(ops, N, X, U, budget_s, threads):
     return {"value": n / dt, "unit": "QP/s", "cores": nthr, "kind": "port",
             "sample": f"{n} QPs of the same batch (first {n} states), oracle/osqp_dense.c fp64, "
                       f"OpenMP {nthr} threads, {dt:.2f} s"}
+
+
+def cpu_baseline_plants(plant, Ad, Bd, N, X, U, budget_s, threads):
+    """The oracle's per-plant path (condense + setup + one controllerStep, fp64 C, OpenMP) on a
+    bounded sample of the config-3 plants."""
+    import oracle
+
+    nthr = threads or min(16, os.cpu_count() or 1)
+    n = 256
+    while True:
+        t0 = time.perf_counter()
+        oracle.plants_step(plant, Ad[:n], Bd[:n], X[:n], U[:n], N, nthreads=nthr)
+        dt = time.perf_counter() - t0
+        if dt > budget_s / 4 or n >= len(X):
+            break
+        n = min(len(X), int(n * max(2.0, budget_s / 4 / max(dt, 1e-3))))
+    return {"value": n / dt, "unit": "QP/s", "cores": nthr, "kind": "port",
+            "sample": f"{n} plants of the same batch (first {n}): oracle/mpc_batch.c condense + osqp_dense.c "
+                      f"setup + solve, fp64, OpenMP {nthr} threads, {dt:.2f} s"}
 
 
 def traffic_per_solve(dtype, batch, N):
@@ -115,9 +139,17 @@ def main():
     l = np.full(2 * N, -np.finfo(np.float64).max)
     u0 = ops["W0"].copy()  # W0 + Sbar 0 + Ku 0 (:43)
 
-    solver = sm.BatchSolver(N, 2 * N, B, 1, a.dtype, local)
-    solver.setup(ops["P"], np.zeros(N), ops["A"], l, u0)
-    solver.mpc_set_operators(ops["Fx"], ops["Fu"], ops["Fr"], ops["Sbar"], ops["Ku"], ops["W0"])
+    perplant = a.workload == "perplant"
+    if perplant:  # config 3: every QP its own plant, condensed and set up on the device each step
+        Ad, Bd = workload.randomized_plants(plant, a.seed, start, count)
+        solver = sm.BatchSolver(N, 2 * N, B, B, a.dtype, local)
+        tdev = lambda v: torch.as_tensor(np.ascontiguousarray(v, dtype=np.float64)).to(dev)  # noqa: E731
+        plant_d = [tdev(Ad), tdev(Bd), tdev(np.tile(plant["Cd"], (B, 1))), tdev(np.tile(plant["K"], (B, 1))),
+                   tdev(np.full(B, plant["Q"])), tdev(np.full(B, plant["R"])), tdev(np.full(B, plant["RD"]))]
+    else:
+        solver = sm.BatchSolver(N, 2 * N, B, 1, a.dtype, local)
+        solver.setup(ops["P"], np.zeros(N), ops["A"], l, u0)
+        solver.mpc_set_operators(ops["Fx"], ops["Fu"], ops["Fr"], ops["Sbar"], ops["Ku"], ops["W0"])
     X_d = torch.from_numpy(X).to(dev)
     U0_d = torch.from_numpy(U).to(dev)
     U_d = U0_d.clone()
@@ -139,11 +171,14 @@ def main():
                                   ctrl_base[0], a.noise, sptr)
             ctrl_base[0] += a.ctrl_steps
         else:
+            if perplant:  # condensing + Ruiz + eigen-basis setup of every plant, on the device
+                solver.mpc_setup_plants_device(4, 10, *[t.data_ptr() for t in plant_d], sptr)
             solver.mpc_step_device(X_d.data_ptr(), U_d.data_ptr(), plant["xref"], sptr)
 
     def reset():
         U_d.copy_(U0_d)          # every step: the reference's first control step of each plant
-        solver.reset_state()     # post-setup solver state (x = z = y = 0, rho = settings.rho)
+        if not perplant:         # (perplant: the setup inside the step resets the state)
+            solver.reset_state()  # post-setup solver state (x = z = y = 0, rho = settings.rho)
         if stream_mode:
             X_d.copy_(X0_d)
             ctrl_base[0] = 0
@@ -188,6 +223,8 @@ def main():
     qps_per_step = B * (a.ctrl_steps if stream_mode else 1)
     # stream: iterations of the last control step stand for every step (estimate, see "flops_note")
     flops = float(workload.flops_per_qp(N, 2 * N, 4, iters).sum()) * (a.ctrl_steps if stream_mode else 1)
+    if perplant:
+        flops += B * workload.flops_plant_setup(N, 2 * N)
     achieved = flops / (kern_ms * 1e-3) / 1e12
     solved = float(np.mean(status == sm.SOLVED))
 
@@ -211,20 +248,26 @@ def main():
         "data": "synthetic (counter-based X ~ N(0, diag(.1,.1,.05,.5)), U ~ U(-1,1); reference plant config)",
         "config": ({"workload": f"cfg2: {B} identical LTI plants per GPU, N={N} (n={N}, m={2 * N}), "
                                 f"one controllerStep each", "batch_per_gpu": B, "horizon": N,
-                    "parallelism": f"dp{world}"} if not stream_mode else
+                    "parallelism": f"dp{world}"} if a.workload == "cfg2" else
+                   {"workload": f"cfg3: {B} randomised plants per GPU (Ad, Bd +-2% ~ N(0,1), rho(Ad) < 1), N={N}: "
+                                f"on-device condensing + setup + one controllerStep each",
+                    "batch_per_gpu": B, "horizon": N, "parallelism": f"dp{world}"} if perplant else
                    {"workload": f"cfg5: {B} plants per GPU x {a.ctrl_steps} warm-started control steps, "
                                 f"simulated plant (noise std {a.noise}), hipGraph-replayed, N={N}",
                     "batch_per_gpu": B, "horizon": N, "ctrl_steps": a.ctrl_steps, "parallelism": f"dp{world}"}),
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS[a.dtype], "unit": "TFLOP/s",
                      "frac": achieved / PEAK_TFLOPS[a.dtype], "traffic": traffic_per_solve(a.dtype, B, N),
-                     "kernel": "admm_tile_kernel (all phase launches of one solve)",
+                     "kernel": ("condense + setup + admm_wave_kernel (whole step)" if perplant else
+                                "admm_tile_kernel (all phase launches of one solve)"),
                      "kernel_ms": kern_ms, "flops_per_solve": flops,
                      "flops_note": "algorithmic: sum over QPs of iters*F_iter + checks*F_check + front end "
                                    "(SURVEY §8d, DESIGN §4.1), actual per-QP iteration counts"
                                    + ("; stream: last control step's counts x ctrl_steps (estimate)" if stream_mode else "")},
         "iters": {"mean": float(iters.mean()), "max": int(iters.max()), "solved_frac": solved},
     }
-    if a.cpu_seconds > 0 and not stream_mode:
+    if a.cpu_seconds > 0 and perplant:
+        rec["cpu_baseline"] = cpu_baseline_plants(plant, Ad, Bd, N, X, U, a.cpu_seconds, a.cpu_threads)
+    elif a.cpu_seconds > 0 and not stream_mode:
         rec["cpu_baseline"] = cpu_baseline(ops, N, X, U, a.cpu_seconds, a.cpu_threads)
     print(json.dumps(rec))
     if dist:

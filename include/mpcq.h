@@ -174,6 +174,16 @@ int mpcq_condense(int device, int n_plants, int nx, int N, int s_rows, const dou
                   const double *R, const double *RD, double *P, double *A, double *Fx, double *Fu,
                   double *Fr, double *Sbar, double *Ku, double *W0);
 
+/* Per-plant condensing + setup on the device (BASELINE config 3): every plant of the context
+ * (n_plants copies, device pointers, plant-major: Ad nx*nx, Bd nx, Cd nx, K nx, Q, R, RD) is
+ * condensed as mpcq_condense does, its front-end operators installed (as mpcq_mpc_set_operators)
+ * and the solver set up on the ctor's data (as mpcq_setup with q0 = 0, l0 = -DBL_MAX, u0 = W0:
+ * ModelPredictiveControlAPI.cpp:22-23,38-43,51-64), all on `stream`; the only host transfer is
+ * the setup's status word.  Needs n == N, m == 2N. */
+int mpcq_mpc_setup_plants_device(mpcq_ctx *ctx, int nx, int s_rows, const double *Ad,
+                                 const double *Bd, const double *Cd, const double *K,
+                                 const double *Q, const double *R, const double *RD, void *stream);
+
 /* Last HIP error string of this thread (static storage). */
 const char *mpcq_last_error(void);
 

@@ -70,7 +70,8 @@ def lib() -> C.CDLL:
     if _LIB is not None:
         return _LIB
     so = _HERE / "liboracle.so"
-    srcs = [_HERE / f for f in ("mpc_condense.c", "osqp_dense.c", "mpc_condense.h", "osqp_dense.h")]
+    srcs = [_HERE / f for f in ("mpc_condense.c", "osqp_dense.c", "mpc_batch.c", "mpc_condense.h", "osqp_dense.h",
+                                "mpc_batch.h")]
     if not so.exists() or any(s.stat().st_mtime > so.stat().st_mtime for s in srcs if s.exists()):
         subprocess.run(["make", "-C", str(_HERE), "-s"], check=True)
     L = C.CDLL(str(so))
@@ -100,6 +101,9 @@ def lib() -> C.CDLL:
     L.ora_condense.argtypes = [C.POINTER(_Plant), C.POINTER(_Ops)]
     L.ora_condense.restype = C.c_int
     L.ora_matpow.argtypes = [C.c_int, dp, C.c_int, dp]
+    L.ora_plants_step.restype = C.c_int
+    L.ora_plants_step.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, dp, dp, dp, dp, C.c_double, C.c_double,
+                                  C.c_double, dp, dp, C.c_double, C.POINTER(Settings), dp, ip, ip, C.c_int]
     _LIB = L
     return L
 
@@ -254,6 +258,23 @@ def batch_solve(P, A, q0, l, u0, q, u, settings: Settings | None = None, nthread
     if rc < 0:
         raise ValueError("ora_batch_solve: setup rejected the data")
     return x, st, it, rho
+
+
+def plants_step(plant: dict, Ad, Bd, X, U, N: int, s_rows: int = 10, xref: float = 0.0,
+                settings: Settings | None = None, nthreads: int = 0):
+    """Per-plant batch (config 3): for plant p with its own Ad[p], Bd[p] (Cd, K, Q, R, RD shared),
+    the reference constructor + one controllerStep from (X[p], U[p]).  Returns (U_new, status, iter)."""
+    Ad, Bd, X, U = _c64(Ad), _c64(Bd), _c64(X), _c64(U)
+    k, nx = Ad.shape[0], Ad.shape[1]
+    Cd, K = _c64(plant["Cd"]), _c64(plant["K"])
+    s = settings or default_settings()
+    U_out = np.zeros(k)
+    st = np.zeros(k, dtype=np.int32)
+    it = np.zeros(k, dtype=np.int32)
+    lib().ora_plants_step(k, nx, N, s_rows, _dp(Ad), _dp(Bd), _dp(Cd), _dp(K), plant["Q"], plant["R"],
+                          plant["RD"], _dp(X), _dp(U), float(xref), C.byref(s), _dp(U_out), _ip(st), _ip(it),
+                          nthreads)
+    return U_out, st, it
 
 
 def kkt_residuals(P, q, A, l, u, x, y) -> dict:

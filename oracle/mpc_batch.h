@@ -1,0 +1,24 @@
+/*
+ * oracle/mpc_batch.h — TEST INFRASTRUCTURE ONLY (CPU checker / CPU baseline, never shipped).
+ * Per-plant condense + setup + one controllerStep (ModelPredictiveControlAPI.cpp:3-65,81-108).
+ */
+#ifndef ORACLE_MPC_BATCH_H
+#define ORACLE_MPC_BATCH_H
+#include "mpc_condense.h"
+#include "osqp_dense.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Plants p = 0..n_plants-1 with their own Ad (nx*nx), Bd (nx); shared Cd, K, Q, R, RD.
+ * X n_plants*nx, U n_plants -> U_out (U + x[0] when solved), status, iters.  Returns failures. */
+int ora_plants_step(int n_plants, int nx, int N, int s_rows, const double *Ad, const double *Bd,
+                    const double *Cd, const double *K, double Q, double R, double RD, const double *X,
+                    const double *U, double xref, const ora_settings *s, double *U_out, int *status,
+                    int *iters, int nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

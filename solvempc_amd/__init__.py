@@ -192,6 +192,16 @@ class BatchSolver:
                                               int(steps), seed, first_qp, first_step, float(noise_std),
                                               C.c_void_p(stream)), "mpcq_mpc_run_device")
 
+    def mpc_setup_plants_device(self, nx: int, s_rows: int, Ad_ptr: int, Bd_ptr: int, Cd_ptr: int, K_ptr: int,
+                                Q_ptr: int, R_ptr: int, RD_ptr: int, stream: int | None = None) -> None:
+        """Condense and set up every plant on the device from device-resident plant data (fp64,
+        plant-major; BASELINE config 3): the per-plant form of mpc.condense + setup +
+        mpc_set_operators, with the ctor's X = U = 0 setup data."""
+        ptrs = [C.c_void_p(p) for p in (Ad_ptr, Bd_ptr, Cd_ptr, K_ptr, Q_ptr, R_ptr, RD_ptr)]
+        _capi.check(lib().mpcq_mpc_setup_plants_device(self._ctx, int(nx), int(s_rows), *ptrs,
+                                                       C.c_void_p(stream or 0)), "mpcq_mpc_setup_plants_device")
+        self.nx = int(nx)
+
     def mpc_step_device(self, X_ptr: int, U_ptr: int, xref: float = 0.0, stream: int | None = None) -> None:
         """Same on device-resident fp64 buffers (e.g. torch tensors' data_ptr()); asynchronous."""
         _capi.check(lib().mpcq_mpc_step_device(self._ctx, C.c_void_p(X_ptr), C.c_void_p(U_ptr),

@@ -18,7 +18,7 @@ EXPORTS = (
     "mpcq_cold_start", "mpcq_reset", "mpcq_solve", "mpcq_get_solution", "mpcq_get_dual", "mpcq_get_info",
     "mpcq_get_scaling", "mpcq_device_view_get", "mpcq_mpc_set_operators", "mpcq_mpc_step_device",
     "mpcq_mpc_step", "mpcq_mpc_set_plant", "mpcq_mpc_simulate_device", "mpcq_mpc_run_device",
-    "mpcq_condense", "mpcq_last_error",
+    "mpcq_condense", "mpcq_mpc_setup_plants_device", "mpcq_last_error",
 )
 
 
@@ -93,6 +93,7 @@ def lib() -> C.CDLL:
         "mpcq_mpc_run_device": (C.c_int, [vp, vp, vp, C.c_double, C.c_int, C.c_ulonglong, C.c_longlong,
                                           C.c_longlong, C.c_double, vp]),
         "mpcq_condense": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int] + [dp] * 15),
+        "mpcq_mpc_setup_plants_device": (C.c_int, [vp, C.c_int, C.c_int] + [vp] * 7 + [vp]),
         "mpcq_last_error": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():

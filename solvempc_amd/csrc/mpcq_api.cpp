@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
@@ -57,6 +58,7 @@ struct mpcq_ctx {
     // setup
     double *d_P = nullptr, *d_q0 = nullptr, *d_A = nullptr, *d_l0 = nullptr, *d_u0 = nullptr;
     double *d_ops = nullptr, *d_scratch = nullptr;
+    int *d_flags = nullptr;
     float *d_ops32 = nullptr;
     int *d_ctype = nullptr, *d_setup_status = nullptr;
     // per QP
@@ -304,6 +306,7 @@ int mpcq_create(const mpcq_dims *d, const mpcq_settings *s, mpcq_ctx **out)
     if (d->dtype == MPCQ_F32) A((void **)&c->d_ops32, 4 * P * L.total);
     A((void **)&c->d_ctype, 4 * P * mc);
     A((void **)&c->d_setup_status, 4 * P);
+    A((void **)&c->d_flags, 4);
     A((void **)&c->d_q, 8 * B * n);
     A((void **)&c->d_u, 8 * B * m);
     A((void **)&c->d_l, 8 * B * m);
@@ -344,7 +347,7 @@ int mpcq_destroy(mpcq_ctx *c)
                     c->d_setup_status, c->d_q, c->d_u, c->d_l, c->d_x, c->d_y, c->d_rho, c->d_status, c->d_iter,
                     c->d_xs, c->d_zs, c->d_ys, c->d_rhos, c->d_snx, c->d_sny, c->d_Fx, c->d_Fu, c->d_Fr,
                     c->d_Sbar, c->d_Ku, c->d_W0, c->d_X, c->d_U, c->d_img, c->d_list, c->d_counts,
-                    c->d_itstate, c->d_Ad, c->d_Bd, c->d_step};
+                    c->d_itstate, c->d_Ad, c->d_Bd, c->d_step, c->d_flags};
     if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
     if (c->graph) (void)hipGraphDestroy(c->graph);
     for (void *p : ptrs)
@@ -353,22 +356,14 @@ int mpcq_destroy(mpcq_ctx *c)
     return MPCQ_OK;
 }
 
-int mpcq_setup(mpcq_ctx *c, const double *P, const double *q0, const double *A, const double *l0,
-               const double *u0)
+// Setup kernels on the device-resident setup data (d_P, d_q0, d_A, d_l0, d_u0), operator
+// conversion / tile images, per-QP broadcast of q0/u0/l0, state reset and the plant-0 scaling
+// readback.  One 4-byte flag word (non-convex plant, non-inequality row) comes back to the host.
+int setup_on_device(mpcq_ctx *c, hipStream_t s)
 {
-    int rc = check_ctx(c, false);
-    if (rc) return rc;
     const size_t Pn = c->dims.n_plants, n = c->dims.n, m = c->dims.m, B = c->dims.batch;
-    if (!P || !q0 || (m && (!A || !l0 || !u0))) return fail(MPCQ_ERR_ARG, "null setup array");
-    for (size_t i = 0; i < Pn * m; i++)
-        if (l0[i] > u0[i]) return fail(MPCQ_ERR_BOUNDS, "lower bound above upper bound (osqp validate_data)");
-    c->setup_done = false;
-    hipStream_t s = c->last;
-    if ((rc = h2d(c->d_P, P, 8 * Pn * n * n, s)) || (rc = h2d(c->d_q0, q0, 8 * Pn * n, s)) ||
-        (rc = h2d(c->d_A, A, 8 * Pn * m * n, s)) || (rc = h2d(c->d_l0, l0, 8 * Pn * m, s)) ||
-        (rc = h2d(c->d_u0, u0, 8 * Pn * m, s)))
-        return rc;
     HIPCHK(hipMemsetAsync(c->d_ops, 0, 8 * Pn * c->ops_stride, s));
+    HIPCHK(hipMemsetAsync(c->d_flags, 0, 4, s));
     mpcq::SetupArgs a{};
     a.n = (int)n;
     a.m = (int)m;
@@ -386,6 +381,7 @@ int mpcq_setup(mpcq_ctx *c, const double *P, const double *q0, const double *A, 
     a.ops = c->d_ops;
     a.ctype = c->d_ctype;
     a.status = c->d_setup_status;
+    a.flags = c->d_flags;
     // one wavefront per plant, LDS-resident (mpcq_setup_wave.hip) where the plant fits; the
     // global-scratch workgroup kernel otherwise (MPCQ_SETUP=ref forces it: A/B test hook)
     const char *se = std::getenv("MPCQ_SETUP");
@@ -395,16 +391,37 @@ int mpcq_setup(mpcq_ctx *c, const double *P, const double *q0, const double *A, 
             return fail(MPCQ_ERR_HIP, "hipMalloc failed (setup scratch)");
         a.scratch = c->d_scratch;
         if (mpcq_internal_setup_launch(&a, s) != 0) return fail(MPCQ_ERR_HIP, "setup kernel launch failed");
-    } else if (mpcq_internal_setup_wave_launch(&a, s) != 0) {
-        return fail(MPCQ_ERR_HIP, "setup kernel launch failed");
+    } else {
+        const char *pe = std::getenv("MPCQ_SETUP_PROF");  // debug hook: per-stage clock stamps to a file
+        long long *prof = nullptr;
+        if (pe && *pe && hipMalloc((void **)&prof, 8 * 16 * Pn) == hipSuccess) {
+            (void)hipMemsetAsync(prof, 0, 8 * 16 * Pn, s);
+            a.prof = prof;
+        }
+        if (mpcq_internal_setup_wave_launch(&a, s) != 0) return fail(MPCQ_ERR_HIP, "setup kernel launch failed");
+        if (prof) {
+            std::vector<long long> h(16 * Pn);
+            HIPCHK(hipMemcpyAsync(h.data(), prof, 8 * 16 * Pn, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            (void)hipFree(prof);
+            if (FILE *f = std::fopen(pe, "wb")) {
+                std::fwrite(h.data(), 8, h.size(), f);
+                std::fclose(f);
+            }
+        }
     }
-    std::vector<int> st(Pn), ct(Pn * c->mc);
-    HIPCHK(hipMemcpyAsync(st.data(), c->d_setup_status, 4 * Pn, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(ct.data(), c->d_ctype, 4 * Pn * c->mc, hipMemcpyDeviceToHost, s));
+    // plant-0 scaling (mpcq_get_scaling, host-side bound checks) and the flag word: one sync
+    const mpcq::OpsLayout L = mpcq::OpsLayout::make(c->nc, c->mc);
+    std::vector<double> blk(c->ops_stride);
+    int flags = 0;
+    HIPCHK(hipMemcpyAsync(&flags, c->d_flags, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(blk.data(), c->d_ops, 8 * c->ops_stride, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    for (size_t p = 0; p < Pn; p++)
-        if (st[p] != 0) return fail(MPCQ_ERR_SETUP, "setup: P + sigma I not positive definite (non-convex QP)");
-    c->all_ineq = std::all_of(ct.begin(), ct.end(), [](int t) { return t == 0; });
+    if (flags & 1) return fail(MPCQ_ERR_SETUP, "setup: P + sigma I not positive definite (non-convex QP)");
+    c->all_ineq = !(flags & 2);
+    for (size_t i = 0; i < n; i++) c->hD[i] = blk[L.D + i];
+    for (size_t j = 0; j < m; j++) c->hE[j] = blk[L.E + j];
+    c->hc = blk[L.cs];
     if (c->dims.dtype == MPCQ_F32 &&
         mpcq_internal_f64_to_f32(c->d_ops, c->d_ops32, Pn * c->ops_stride, s) != 0)
         return fail(MPCQ_ERR_HIP, "operator conversion failed");
@@ -416,15 +433,25 @@ int mpcq_setup(mpcq_ctx *c, const double *P, const double *q0, const double *A, 
         mpcq_internal_broadcast(c->d_u0, c->d_u, (int)m, (int)B, per, s) ||
         mpcq_internal_broadcast(c->d_l0, c->d_l, (int)m, (int)B, per, s))
         return fail(MPCQ_ERR_HIP, "broadcast failed");
-    if ((rc = reset_state(c, true))) return rc;
-    // plant-0 scaling, for mpcq_get_scaling and host-side bound validation
-    const mpcq::OpsLayout L = mpcq::OpsLayout::make(c->nc, c->mc);
-    std::vector<double> blk(c->ops_stride);
-    HIPCHK(hipMemcpyAsync(blk.data(), c->d_ops, 8 * c->ops_stride, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    for (size_t i = 0; i < n; i++) c->hD[i] = blk[L.D + i];
-    for (size_t j = 0; j < m; j++) c->hE[j] = blk[L.E + j];
-    c->hc = blk[L.cs];
+    return reset_state(c, true);
+}
+
+int mpcq_setup(mpcq_ctx *c, const double *P, const double *q0, const double *A, const double *l0,
+               const double *u0)
+{
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    const size_t Pn = c->dims.n_plants, n = c->dims.n, m = c->dims.m;
+    if (!P || !q0 || (m && (!A || !l0 || !u0))) return fail(MPCQ_ERR_ARG, "null setup array");
+    for (size_t i = 0; i < Pn * m; i++)
+        if (l0[i] > u0[i]) return fail(MPCQ_ERR_BOUNDS, "lower bound above upper bound (osqp validate_data)");
+    c->setup_done = false;
+    hipStream_t s = c->last;
+    if ((rc = h2d(c->d_P, P, 8 * Pn * n * n, s)) || (rc = h2d(c->d_q0, q0, 8 * Pn * n, s)) ||
+        (rc = h2d(c->d_A, A, 8 * Pn * m * n, s)) || (rc = h2d(c->d_l0, l0, 8 * Pn * m, s)) ||
+        (rc = h2d(c->d_u0, u0, 8 * Pn * m, s)))
+        return rc;
+    if ((rc = setup_on_device(c, s))) return rc;
     c->lower_free = lower_all_free(c, l0);
     c->setup_done = true;
     return MPCQ_OK;
@@ -686,6 +713,23 @@ int mpcq_device_view_get(mpcq_ctx *c, mpcq_device_view *v)
     return MPCQ_OK;
 }
 
+// Device buffers of the MPC front-end operators for nx states (per plant) and X/U staging.
+bool alloc_mpc_ops(mpcq_ctx *c, int nx)
+{
+    const size_t Pn = c->dims.n_plants, n = c->dims.n, m = c->dims.m;
+    if (c->nx != nx) {
+        for (double **p : {&c->d_Fx, &c->d_Sbar})
+            if (*p) { (void)hipFree(*p); *p = nullptr; }
+        if (c->d_X) { (void)hipFree(c->d_X); c->d_X = nullptr; }
+    }
+    auto A = [&](double **p, size_t cnt) -> bool {
+        return *p || hipMalloc((void **)p, 8 * std::max<size_t>(cnt, 1)) == hipSuccess;
+    };
+    return A(&c->d_Fx, Pn * n * nx) && A(&c->d_Fu, Pn * n) && A(&c->d_Fr, Pn * n * n) &&
+           A(&c->d_Sbar, Pn * m * nx) && A(&c->d_Ku, Pn * m) && A(&c->d_W0, Pn * m) &&
+           A(&c->d_X, (size_t)c->dims.batch * nx) && A(&c->d_U, (size_t)c->dims.batch);
+}
+
 int mpcq_mpc_set_operators(mpcq_ctx *c, int nx, const double *Fx, const double *Fu, const double *Fr,
                            const double *Sbar, const double *Ku, const double *W0)
 {
@@ -695,17 +739,7 @@ int mpcq_mpc_set_operators(mpcq_ctx *c, int nx, const double *Fx, const double *
     if (nx <= 0 || nx > 8) return fail(MPCQ_ERR_ARG, "nx must be in 1..8");
     if (m != 2 * n) return fail(MPCQ_ERR_ARG, "MPC front end needs m == 2n (ModelPredictiveControlAPI.cpp:47-48)");
     if (!Fx || !Fu || !Fr || !Sbar || !Ku || !W0) return fail(MPCQ_ERR_ARG, "null operator");
-    if (c->nx != nx) {
-        for (double **p : {&c->d_Fx, &c->d_Sbar})
-            if (*p) { (void)hipFree(*p); *p = nullptr; }
-    }
-    auto A = [&](double **p, size_t cnt) -> bool {
-        return *p || hipMalloc((void **)p, 8 * std::max<size_t>(cnt, 1)) == hipSuccess;
-    };
-    if (!A(&c->d_Fx, Pn * n * nx) || !A(&c->d_Fu, Pn * n) || !A(&c->d_Fr, Pn * n * n) ||
-        !A(&c->d_Sbar, Pn * m * nx) || !A(&c->d_Ku, Pn * m) || !A(&c->d_W0, Pn * m) ||
-        !A(&c->d_X, (size_t)c->dims.batch * 8) || !A(&c->d_U, (size_t)c->dims.batch))
-        return fail(MPCQ_ERR_HIP, "hipMalloc failed");
+    if (!alloc_mpc_ops(c, nx)) return fail(MPCQ_ERR_HIP, "hipMalloc failed");
     c->nx = nx;
     hipStream_t s = c->last;
     if ((rc = h2d(c->d_Fx, Fx, 8 * Pn * n * nx, s)) || (rc = h2d(c->d_Fu, Fu, 8 * Pn * n, s)) ||
@@ -846,7 +880,9 @@ int mpcq_condense(int device, int n_plants, int nx, int N, int s_rows, const dou
     const size_t Pn = n_plants, X = nx, n = N;
     const size_t in_cnt[] = {Pn * X * X, Pn * X, Pn * X, Pn * X, Pn, Pn, Pn};
     const size_t out_cnt[] = {Pn * n * n, Pn * 2 * n * n, Pn * n * X, Pn * n, Pn * n * n, Pn * 2 * n * X, Pn * 2 * n, Pn * 2 * n};
-    const size_t scr = Pn * mpcq_internal_condense_scratch(nx, N);
+    const char *ce = std::getenv("MPCQ_CONDENSE");  // test hook: "ref" forces the workgroup kernel
+    const bool force_ref = ce && !std::strcmp(ce, "ref");
+    const size_t scr = (N > 32 || force_ref) ? Pn * mpcq_internal_condense_scratch(nx, N) : 0;
     size_t total = scr;
     for (size_t c : in_cnt) total += c;
     for (size_t c : out_cnt) total += c;
@@ -866,7 +902,8 @@ int mpcq_condense(int device, int n_plants, int nx, int N, int s_rows, const dou
         *dout[i] = p;
         p += out_cnt[i];
     }
-    a.scratch = p;
+    a.scratch = scr ? p : nullptr;
+    a.force_ref = force_ref;
     a.n_plants = n_plants;
     a.nx = nx;
     a.N = N;
@@ -878,6 +915,46 @@ int mpcq_condense(int device, int n_plants, int nx, int N, int s_rows, const dou
             rc = fail(MPCQ_ERR_HIP, "d2h");
     (void)hipFree(buf);
     return rc;
+}
+
+
+int mpcq_mpc_setup_plants_device(mpcq_ctx *c, int nx, int s_rows, const double *Ad, const double *Bd,
+                                 const double *Cd, const double *K, const double *Q, const double *R,
+                                 const double *RD, void *stream)
+{
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    const size_t Pn = c->dims.n_plants, n = c->dims.n, m = c->dims.m;
+    if (nx <= 0 || nx > 8 || s_rows < 0) return fail(MPCQ_ERR_ARG, "setup_plants: 1 <= nx <= 8, s_rows >= 0");
+    if (m != 2 * n) return fail(MPCQ_ERR_ARG, "MPC front end needs m == 2n (ModelPredictiveControlAPI.cpp:47-48)");
+    if (!Ad || !Bd || !Cd || !K || !Q || !R || !RD) return fail(MPCQ_ERR_ARG, "setup_plants: null plant array");
+    if (!alloc_mpc_ops(c, nx)) return fail(MPCQ_ERR_HIP, "hipMalloc failed");
+    c->nx = nx;
+    c->setup_done = false;
+    hipStream_t s = (hipStream_t)stream;
+    c->last = s;
+    mpcq::CondenseArgs a{};
+    a.n_plants = (int)Pn;
+    a.nx = nx;
+    a.N = (int)n;
+    a.s_rows = s_rows;
+    a.Ad = Ad; a.Bd = Bd; a.Cd = Cd; a.K = K; a.Q = Q; a.R = R; a.RD = RD;
+    a.P = c->d_P; a.A = c->d_A;
+    a.Fx = c->d_Fx; a.Fu = c->d_Fu; a.Fr = c->d_Fr; a.Sbar = c->d_Sbar; a.Ku = c->d_Ku; a.W0 = c->d_W0;
+    a.q0 = c->d_q0; a.l0 = c->d_l0; a.u0 = c->d_u0;
+    double *scr = nullptr;
+    if (n > 32 && hipMalloc((void **)&scr, 8 * Pn * mpcq_internal_condense_scratch(nx, (int)n)) != hipSuccess)
+        return fail(MPCQ_ERR_HIP, "hipMalloc failed (condense scratch)");
+    a.scratch = scr;
+    rc = mpcq_internal_condense_launch(&a, s) != 0 ? fail(MPCQ_ERR_HIP, "condense launch failed") : MPCQ_OK;
+    if (!rc) rc = setup_on_device(c, s);
+    if (scr) (void)hipFree(scr);
+    if (rc) return rc;
+    c->last = s;
+    c->lower_free = true;  // l0 = -DBL_MAX on every row (:42)
+    c->mpc_ready = true;
+    c->setup_done = true;
+    return MPCQ_OK;
 }
 
 }  // extern "C"

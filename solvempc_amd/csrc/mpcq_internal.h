@@ -105,6 +105,8 @@ struct SetupArgs {
     int *ctype;        // [plant] mc
     double *scratch;   // [plant] scratch_len(n, m)
     int *status;       // [plant] 0 ok, else error
+    long long *prof;   // debug (MPCQ_SETUP_PROF): [plant][16] stage clock stamps, or null
+    int *flags;        // OR over plants: 1 setup failed (non-convex), 2 a row is not an inequality
 };
 
 // Arguments of the ADMM kernel (one QP per lane).
@@ -187,7 +189,9 @@ struct CondenseArgs {
     int n_plants, nx, N, s_rows;
     const double *Ad, *Bd, *Cd, *K, *Q, *R, *RD;  // [plant] nx*nx, nx, nx, nx, 1, 1, 1
     double *P, *A, *Fx, *Fu, *Fr, *Sbar, *Ku, *W0;  // [plant] N*N, 2N*N, N*nx, N, N*N, 2N*nx, 2N, 2N
-    double *scratch;                                 // [plant] condense_scratch_len
+    double *scratch;                                 // [plant] condense_scratch_len (N > 32 only)
+    double *q0, *l0, *u0;                            // optional: the ctor's setup data (0, -DBL_MAX, W0)
+    int force_ref;                                   // test hook: the workgroup kernel at any N
 };
 }  // namespace mpcq
 

@@ -120,6 +120,7 @@ __global__ __launch_bounds__(64) void setup_kernel(SetupArgs a)
         else { ty = 0; rs = 1.0; }
         ctype[i] = ty;
         Et[i] = rs;  // reuse Et as rscale
+        if (ty != 0) atomicOr(a.flags, 2);
     }
     __syncthreads();
 
@@ -282,7 +283,10 @@ __global__ __launch_bounds__(64) void setup_kernel(SetupArgs a)
         o_Ah[e] = ah;
     }
     __syncthreads();
-    if (t == 0) a.status[p] = fail ? kNonCvx : 0;
+    if (t == 0) {
+        a.status[p] = fail ? kNonCvx : 0;
+        if (fail) atomicOr(a.flags, 1);
+    }
 }
 
 __global__ void f64_to_f32_kernel(const double *in, float *out, size_t count)

@@ -17,6 +17,10 @@
 
 namespace mpcq {
 
+// Debug hook (MPCQ_SETUP_PROF): per-plant shader-clock stamps at the stage boundaries.
+#define MPCQ_STAMP(k) \
+    do { if (a.prof && t == 0) a.prof[(size_t)pl * 16 + (k)] = (long long)clock64(); } while (0)
+
 struct SetupWaveShape {
     int n, m, ne, ld;
     size_t Ph, Ah, L, T, C, V, Dv, Ev, Dt, Et, qh, rot, total;  // offsets in doubles
@@ -87,6 +91,7 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
     double *out = a.ops + (size_t)pl * Lo.total;
     int *ctype = a.ctype + (size_t)pl * mc;
 
+    MPCQ_STAMP(0);
     // ---- data (osqp-eigen keeps the upper triangle of the Hessian)
     for (int e = t; e < n * n; e += 64) {
         const int i = e / n, j = e % n;
@@ -98,6 +103,7 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
     if (t == 0) sh[0] = 1.0;
     __syncthreads();
 
+    MPCQ_STAMP(1);
     // ---- Ruiz equilibration + cost normalisation (OSQP scale_data)
     for (int it = 0; it < a.scaling; it++) {
         if (t < n) {
@@ -147,6 +153,7 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
     }
     const double cost = sh[0];
 
+    MPCQ_STAMP(2);
     // ---- constraint types from the scaled setup bounds (OSQP set_rho_vec); Et <- rscale
     for (int i = t; i < m; i += 64) {
         const double lo = l0[i] * Ev[i], up = u0[i] * Ev[i];
@@ -157,10 +164,12 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
         else { ty = 0; rs = 1.0; }
         ctype[i] = ty;
         Et[i] = rs;
+        if (ty != 0) atomicOr(a.flags, 2);
     }
     for (int i = m + t; i < mc; i += 64) ctype[i] = 0;
     __syncthreads();
 
+    MPCQ_STAMP(3);
     // ---- P~ = P^ + sigma I + RHO_MIN sum_free a a' (into L), G = sum rscale a a' (into Tm)
     for (int e = t; e < n * n; e += 64) {
         const int i = e / n, k = e % n;
@@ -176,6 +185,7 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
     }
     __syncthreads();
 
+    MPCQ_STAMP(4);
     // ---- Cholesky P~ = L L' in place (right-looking; upper triangle zeroed at the end)
     int fail = 0;
     for (int j = 0; j < n; j++) {
@@ -199,6 +209,7 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
     }
     __syncthreads();
 
+    MPCQ_STAMP(5);
     // ---- C = L^-1 G L^-T: Tm <- L^-1 G (row steps), C <- Tm', C <- L^-1 C, symmetrise
     for (int i = 0; i < n; i++) {
         const double li = L[i * ld + i];
@@ -236,6 +247,7 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
     }
     __syncthreads();
 
+    MPCQ_STAMP(6);
     // ---- parallel-ordering Jacobi: C = V diag(lambda) V'
     const int np = ne / 2, nblk = np * (np + 1) / 2;
     for (int sweep = 0; sweep < 60 && ne > 1; sweep++) {
@@ -247,6 +259,7 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
         }
         off = wave_sum(off);
         dia = wave_sum(dia);
+        if (a.prof && t == 0) a.prof[(size_t)pl * 16 + 15] = sweep;
         if (off <= 1e-32 * dia || off < 1e-300) break;
         for (int r = 0; r < ne - 1; r++) {
             if (t < np) {
@@ -304,6 +317,7 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
         }
     }
 
+    MPCQ_STAMP(7);
     // ---- W^-1 = V' L' (needs V before it is overwritten), then W = L^-T V in place on V
     double *o_lam = out + Lo.lam, *o_W = out + Lo.W, *o_sWtW = out + Lo.sWtW, *o_WtA = out + Lo.WtA;
     double *o_PW = out + Lo.PW, *o_Winv = out + Lo.Winv, *o_Ah = out + Lo.Ah, *o_D = out + Lo.D, *o_E = out + Lo.E;
@@ -363,7 +377,11 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
         o_WtA[e] = b;
         o_Ah[e] = ah;
     }
-    if (t == 0) a.status[pl] = fail ? kNonCvx : 0;
+    MPCQ_STAMP(8);
+    if (t == 0) {
+        a.status[pl] = fail ? kNonCvx : 0;
+        if (fail) atomicOr(a.flags, 1);
+    }
 }
 
 }  // namespace mpcq

@@ -21,10 +21,12 @@ def _splitmix64(x: np.ndarray) -> np.ndarray:
         return z ^ (z >> np.uint64(31))
 
 
-def uniforms(seed: int, start: int, count: int, draws: int, draw0: int = 0) -> np.ndarray:
-    """(count, draws) uniforms in (0, 1) for global QP indices start .. start+count-1 (draw indices
-    draw0 .. draw0+draws-1; mpcq_stream.hip's device generator is the same function)."""
-    idx = np.arange(start, start + count, dtype=np.uint64)[:, None]
+def uniforms(seed: int, start: int, count: int, draws: int, draw0: int = 0, idx=None) -> np.ndarray:
+    """(count, draws) uniforms in (0, 1) for global QP indices start .. start+count-1 (or the index
+    array `idx`; draw indices draw0 .. draw0+draws-1; mpcq_stream.hip's device generator is the same
+    function)."""
+    idx = (np.arange(start, start + count, dtype=np.uint64) if idx is None
+           else np.asarray(idx, dtype=np.uint64))[:, None]
     d = np.arange(draw0, draw0 + draws, dtype=np.uint64)[None, :]
     with np.errstate(over="ignore"):
         key = _splitmix64(np.uint64(seed) * np.uint64(0x632BE59BD9B4E019) + np.uint64(1))
@@ -64,6 +66,31 @@ def mpc_states(seed: int, start: int, count: int, u_range: float = 1.0):
     return X, U
 
 
+def randomized_plants(plant: dict, seed: int, start: int, count: int, rel: float = 0.02, attempts: int = 64):
+    """Config 3 plants for global indices start .. start+count-1: Ad = Ad0 o (1 + rel eps),
+    Bd = Bd0 o (1 + rel eps), eps ~ N(0, 1) (Box-Muller on draws 32a .. 32a+19 of attempt a); a draw
+    with spectral radius rho(Ad) >= 1 is rejected and redrawn (after `attempts` the nominal plant)."""
+    Ad0, Bd0 = np.asarray(plant["Ad"], dtype=np.float64), np.asarray(plant["Bd"], dtype=np.float64)
+    nx = Ad0.shape[0]
+    k = nx * nx + nx
+    Ad = np.broadcast_to(Ad0, (count, nx, nx)).copy()
+    Bd = np.broadcast_to(Bd0, (count, nx)).copy()
+    todo = np.arange(count)
+    for a in range(attempts):
+        if todo.size == 0:
+            break
+        u = uniforms(seed, 0, 0, 2 * ((k + 1) // 2), draw0=32 * a, idx=start + todo)
+        r = np.sqrt(-2.0 * np.log(u[:, 0::2]))
+        th = 2.0 * np.pi * u[:, 1::2]
+        eps = np.concatenate([r * np.cos(th), r * np.sin(th)], axis=1)[:, :k]
+        cA = Ad0[None] * (1 + rel * eps[:, :nx * nx].reshape(-1, nx, nx))
+        cB = Bd0[None] * (1 + rel * eps[:, nx * nx:])
+        ok = np.abs(np.linalg.eigvals(cA)).max(axis=1) < 1.0
+        Ad[todo[ok]], Bd[todo[ok]] = cA[ok], cB[ok]
+        todo = todo[~ok]
+    return Ad, Bd
+
+
 def shard(total: int, rank: int, world: int) -> tuple[int, int]:
     """Contiguous block [start, start+count) of a global index range for one rank."""
     base, rem = divmod(total, world)
@@ -99,3 +126,11 @@ def flops_per_qp(n: int, m: int, nx: int, iters: np.ndarray, check: int = 25) ->
     f_check = 4 * n * m + 2 * n * n + 6 * m + 4 * n
     f_front = 2 * n * (nx + 1 + n) + 2 * m * (nx + 1) + 2 * n * n
     return it * f_iter + np.floor(it / check) * f_check + f_front
+
+
+def flops_plant_setup(n: int, m: int, N: int | None = None) -> float:
+    """Algorithmic FLOPs of one plant's condensing + setup: F_condense (SISO)
+    4N^3 + 10N^2 + 128N, Ruiz 10*3(n^2 + nm), F_setup 2n^2 m + n^3/3 + n^2 (one LDL of the KKT
+    system; the eigen-basis setup does more work than this and is not credited for it)."""
+    N = n if N is None else N
+    return (4 * N ** 3 + 10 * N ** 2 + 128 * N) + 30 * (n * n + n * m) + (2 * n * n * m + n ** 3 / 3 + n * n)

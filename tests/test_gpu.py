@@ -411,3 +411,64 @@ def test_setup_wave_vs_workgroup_kernel(n, m):
         assert stw[b] == st_o[0] and itw[b] == it_o[0], b
         assert np.abs(xw[b] - x_o[0]).max() < 1e-8
     assert np.array_equal(stw, str_) and np.abs(xw - xr).max() < 1e-8
+
+
+def _perturbed_plants(plant, B, seed):
+    rng = np.random.default_rng(seed)
+    Ad = plant["Ad"][None] * (1 + 0.02 * rng.normal(size=(B, 4, 4)))
+    Bd = plant["Bd"][None] * (1 + 0.02 * rng.normal(size=(B, 4)))
+    return Ad, Bd
+
+
+def test_condense_wave_kernel_bit_identical(plant):
+    """The one-wave LDS condensing kernel reproduces the workgroup kernel bit for bit (same
+    arithmetic order), on perturbed plants and both horizons of the fixtures."""
+    B = 32
+    Ad, Bd = _perturbed_plants(plant, B, 11)
+    pl = {"Ad": Ad, "Bd": Bd, "Cd": np.tile(plant["Cd"], (B, 1)), "K": np.tile(plant["K"], (B, 1)),
+          "Q": np.full(B, plant["Q"]), "R": np.full(B, plant["R"]), "RD": np.full(B, plant["RD"])}
+    for N in (15, 20, 32):
+        dev = sm.mpc.condense(pl, N)
+        os.environ["MPCQ_CONDENSE"] = "ref"
+        try:
+            ref = sm.mpc.condense(pl, N)
+        finally:
+            os.environ.pop("MPCQ_CONDENSE", None)
+        for k in dev:
+            assert np.array_equal(dev[k], ref[k]), (N, k)
+
+
+def test_per_plant_device_pipeline(plant):
+    """BASELINE config 3 path: randomised plants resident on the device -> on-device condensing and
+    setup (mpcq_mpc_setup_plants_device) -> device front end and solve (mpcq_mpc_step_device), against
+    the oracle's condense + controllerStep for every plant."""
+    import torch
+
+    N, B = 20, 96
+    Ad, Bd = _perturbed_plants(plant, B, 7)
+    X, U = workload.mpc_states(3, 0, B)
+    dev = torch.device("cuda:0")
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64), device=dev)  # noqa: E731
+    tAd, tBd = t(Ad), t(Bd)
+    tCd, tK = t(np.tile(plant["Cd"], (B, 1))), t(np.tile(plant["K"], (B, 1)))
+    tQ, tR, tRD = t(np.full(B, plant["Q"])), t(np.full(B, plant["R"])), t(np.full(B, plant["RD"]))
+    tX, tU = t(X), t(U)
+    s = sm.BatchSolver(N, 2 * N, B, n_plants=B)
+    stream = torch.cuda.current_stream().cuda_stream
+    s.mpc_setup_plants_device(4, 10, tAd.data_ptr(), tBd.data_ptr(), tCd.data_ptr(), tK.data_ptr(),
+                              tQ.data_ptr(), tR.data_ptr(), tRD.data_ptr(), stream)
+    s.mpc_step_device(tX.data_ptr(), tU.data_ptr(), 0.0, stream)
+    torch.cuda.synchronize()
+    st, it, _ = s.info()
+    Ug = tU.cpu().numpy()
+    for b in range(B):
+        pl = dict(plant, Ad=Ad[b], Bd=Bd[b])
+        ops = oracle.condense(pl, N)
+        l = np.full(2 * N, LMIN)
+        r = oracle.Solver(ops["P"], np.zeros(N), ops["A"], l, oracle.upper_bound(ops, np.zeros(4), 0.0))
+        assert r.update_gradient(oracle.gradient(ops, X[b], U[b]))
+        assert r.update_upper_bound(oracle.upper_bound(ops, X[b], U[b]))
+        st_o = r.solve()
+        assert st[b] == st_o and it[b] == r.info().iter, b
+        u_ref = U[b] + (r.x()[0] if st_o == sm.SOLVED else 0.0)
+        assert abs(Ug[b] - u_ref) < 1e-9, b

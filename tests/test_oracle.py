@@ -124,3 +124,27 @@ def test_max_iter_and_warm_start(plant):
     s2.update_gradient(q)
     s2.update_upper_bound(u)
     assert s2.solve() == oracle.SOLVED and s2.info().iter == 25
+
+
+def test_plants_step_matches_per_plant_solver(plant):
+    """oracle.plants_step (config-3 CPU path / baseline) == condense + Solver per plant; the
+    randomised plants are shard-invariant and stable."""
+    from solvempc_amd import workload
+
+    B, N = 24, 20
+    Ad, Bd = workload.randomized_plants(plant, 2, 100, B)
+    A2, B2 = workload.randomized_plants(plant, 2, 110, 4)
+    assert np.array_equal(A2, Ad[10:14]) and np.array_equal(B2, Bd[10:14])
+    assert np.abs(np.linalg.eigvals(Ad)).max() < 1.0
+    X, U = workload.mpc_states(3, 0, B)
+    Uo, st, it = oracle.plants_step(plant, Ad, Bd, X, U, N, nthreads=2)
+    for b in range(B):
+        ops = oracle.condense(dict(plant, Ad=Ad[b], Bd=Bd[b]), N)
+        r = oracle.Solver(ops["P"], np.zeros(N), ops["A"], np.full(2 * N, -np.finfo(np.float64).max),
+                          oracle.upper_bound(ops, np.zeros(4), 0.0))
+        assert r.update_gradient(oracle.gradient(ops, X[b], U[b]))
+        assert r.update_upper_bound(oracle.upper_bound(ops, X[b], U[b]))
+        s = r.solve()
+        assert st[b] == s and it[b] == r.info().iter
+        # (numpy's q/u products round differently from the C loops in the last bits)
+        assert abs(Uo[b] - (U[b] + r.x()[0] if s == 1 else U[b])) < 1e-12
