@@ -250,6 +250,13 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
     MPCQ_STAMP(6);
     // ---- parallel-ordering Jacobi: C = V diag(lambda) V'
     const int np = ne / 2, nblk = np * (np + 1) / 2;
+    // Block b = t of the upper-triangular pair grid, decoded once (the grid is the same every round).
+    int bu0 = 0, bv0 = 0;
+    {
+        int bb = t;
+        while (bu0 < np && bb >= np - bu0) { bb -= np - bu0; bu0++; }
+        bv0 = bu0 + bb;
+    }
     for (int sweep = 0; sweep < 60 && ne > 1; sweep++) {
         double off = 0.0, dia = 0.0;
         for (int e = t; e < n * n; e += 64) {
@@ -281,9 +288,13 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
             }
             __syncthreads();
             for (int b = t; b < nblk; b += 64) {
-                int u = 0, bb = b;
-                while (bb >= np - u) { bb -= np - u; u++; }
-                const int v = u + bb;
+                int u = bu0, v = bv0;
+                if (b != t) {
+                    int bb = b;
+                    u = 0;
+                    while (bb >= np - u) { bb -= np - u; u++; }
+                    v = u + bb;
+                }
                 const int pu = (int)rot[5 * u + 4] & 255, qu = (int)rot[5 * u + 4] >> 8;
                 if (u == v) {
                     C[pu * ld + pu] = rot[5 * u + 2];
