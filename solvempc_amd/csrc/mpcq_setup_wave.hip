@@ -251,6 +251,7 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
     // ---- parallel-ordering Jacobi: C = V diag(lambda) V'
     const int np = ne / 2, nblk = np * (np + 1) / 2;
     // Block b = t of the upper-triangular pair grid, decoded once (the grid is the same every round).
+    const int dq64 = np > 0 ? 64 / np : 0, dr64 = np > 0 ? 64 % np : 0;  // (row, u) step of the V-update walk (e += 64)
     int bu0 = 0, bv0 = 0;
     {
         int bb = t;
@@ -316,13 +317,14 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
                     C[qu * ld + qv] = z11; C[qv * ld + qu] = z11;
                 }
             }
-            for (int e = t; e < n * np; e += 64) {
-                const int row = e / np, u = e % np;
+            for (int e = t, row = t / np, u = t % np; e < n * np; e += 64) {
                 const int pu = (int)rot[5 * u + 4] & 255, qu = (int)rot[5 * u + 4] >> 8;
                 const double cu = rot[5 * u], su = rot[5 * u + 1];
                 const double vp = V[row * ld + pu], vq = V[row * ld + qu];
                 V[row * ld + pu] = cu * vp - su * vq;
                 V[row * ld + qu] = su * vp + cu * vq;
+                row += dq64; u += dr64;
+                if (u >= np) { u -= np; row++; }
             }
             __syncthreads();
         }
