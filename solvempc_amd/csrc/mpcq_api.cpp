@@ -74,7 +74,11 @@ struct mpcq_ctx {
     int plant_nx = 0;
     hipGraph_t graph = nullptr;
     hipGraphExec_t gexec = nullptr;
-    struct { double *X, *U; double xref, noise; unsigned long long seed; long long first_qp; hipStream_t s; } gkey{};
+    // gen: bumped whenever buffers baked into the captured graph are reallocated or the kernel
+    // variant flags (all_ineq, lower_free) may change; a replay needs the generation it captured
+    unsigned long long gen = 1;
+    struct { double *X, *U; double xref, noise; unsigned long long seed; long long first_qp; hipStream_t s;
+             unsigned long long gen; } gkey{};
     // host copies of plant-0 scaling
     std::vector<double> hD, hE;
     double hc = 1.0;
@@ -361,6 +365,7 @@ int mpcq_destroy(mpcq_ctx *c)
 // readback.  One 4-byte flag word (non-convex plant, non-inequality row) comes back to the host.
 int setup_on_device(mpcq_ctx *c, hipStream_t s)
 {
+    c->gen++;
     const size_t Pn = c->dims.n_plants, n = c->dims.n, m = c->dims.m, B = c->dims.batch;
     HIPCHK(hipMemsetAsync(c->d_ops, 0, 8 * Pn * c->ops_stride, s));
     HIPCHK(hipMemsetAsync(c->d_flags, 0, 4, s));
@@ -407,6 +412,8 @@ int setup_on_device(mpcq_ctx *c, hipStream_t s)
             if (FILE *f = std::fopen(pe, "wb")) {
                 std::fwrite(h.data(), 8, h.size(), f);
                 std::fclose(f);
+            } else {
+                std::fprintf(stderr, "[mpcq] MPCQ_SETUP_PROF: cannot open %s for writing\n", pe);
             }
         }
     }
@@ -418,6 +425,7 @@ int setup_on_device(mpcq_ctx *c, hipStream_t s)
     HIPCHK(hipMemcpyAsync(blk.data(), c->d_ops, 8 * c->ops_stride, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     if (flags & 1) return fail(MPCQ_ERR_SETUP, "setup: P + sigma I not positive definite (non-convex QP)");
+    if (flags & 4) return fail(MPCQ_ERR_SETUP, "setup: Jacobi eigen-solve of the KKT family did not converge in 60 sweeps");
     c->all_ineq = !(flags & 2);
     for (size_t i = 0; i < n; i++) c->hD[i] = blk[L.D + i];
     for (size_t j = 0; j < m; j++) c->hE[j] = blk[L.E + j];
@@ -453,6 +461,7 @@ int mpcq_setup(mpcq_ctx *c, const double *P, const double *q0, const double *A, 
         return rc;
     if ((rc = setup_on_device(c, s))) return rc;
     c->lower_free = lower_all_free(c, l0);
+    c->gen++;
     c->setup_done = true;
     return MPCQ_OK;
 }
@@ -478,7 +487,9 @@ int mpcq_update_lower_bound(mpcq_ctx *c, const double *l)
     int rc = check_ctx(c, true);
     if (rc) return rc;
     if (!l) return fail(MPCQ_ERR_ARG, "null l");
-    c->lower_free = lower_all_free_batch(c, l);
+    const bool lf = lower_all_free_batch(c, l);
+    if (lf != c->lower_free) c->gen++;
+    c->lower_free = lf;
     return h2d(c->d_l, l, 8 * (size_t)c->dims.batch * c->dims.m, c->last);
 }
 
@@ -718,6 +729,7 @@ bool alloc_mpc_ops(mpcq_ctx *c, int nx)
 {
     const size_t Pn = c->dims.n_plants, n = c->dims.n, m = c->dims.m;
     if (c->nx != nx) {
+        c->gen++;
         for (double **p : {&c->d_Fx, &c->d_Sbar})
             if (*p) { (void)hipFree(*p); *p = nullptr; }
         if (c->d_X) { (void)hipFree(c->d_X); c->d_X = nullptr; }
@@ -777,6 +789,7 @@ int mpcq_mpc_set_plant(mpcq_ctx *c, int nx, const double *Ad, const double *Bd)
     if (nx <= 0 || nx > 8 || !Ad || !Bd) return fail(MPCQ_ERR_ARG, "set_plant: 1 <= nx <= 8 and Ad, Bd required");
     const size_t Pn = c->dims.n_plants;
     if (c->plant_nx != nx) {
+        c->gen++;
         for (double **p : {&c->d_Ad, &c->d_Bd})
             if (*p) { (void)hipFree(*p); *p = nullptr; }
     }
@@ -835,7 +848,7 @@ int mpcq_mpc_run_device(mpcq_ctx *c, double *X, double *U, double xref, int step
     }
     const bool same = c->gexec && c->gkey.X == X && c->gkey.U == U && c->gkey.xref == xref &&
                       c->gkey.noise == noise_std && c->gkey.seed == seed && c->gkey.first_qp == first_qp &&
-                      c->gkey.s == s;
+                      c->gkey.s == s && c->gkey.gen == c->gen;
     if (!same && done < steps) {
         if (c->gexec) { (void)hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
         if (c->graph) { (void)hipGraphDestroy(c->graph); c->graph = nullptr; }
@@ -851,7 +864,7 @@ int mpcq_mpc_run_device(mpcq_ctx *c, double *X, double *U, double xref, int step
         if (ec != hipSuccess) return fail(MPCQ_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ec));
         c->graph = g;
         HIPCHK(hipGraphInstantiate(&c->gexec, c->graph, nullptr, nullptr, 0));
-        c->gkey = {X, U, xref, noise_std, seed, first_qp, s};
+        c->gkey = {X, U, xref, noise_std, seed, first_qp, s, c->gen};
     }
     for (int k = done; k < steps; k++) {
         HIPCHK(hipGraphLaunch(c->gexec, s));
@@ -952,6 +965,7 @@ int mpcq_mpc_setup_plants_device(mpcq_ctx *c, int nx, int s_rows, const double *
     if (rc) return rc;
     c->last = s;
     c->lower_free = true;  // l0 = -DBL_MAX on every row (:42)
+    c->gen++;
     c->mpc_ready = true;
     c->setup_done = true;
     return MPCQ_OK;

@@ -106,7 +106,8 @@ struct SetupArgs {
     double *scratch;   // [plant] scratch_len(n, m)
     int *status;       // [plant] 0 ok, else error
     long long *prof;   // debug (MPCQ_SETUP_PROF): [plant][16] stage clock stamps, or null
-    int *flags;        // OR over plants: 1 setup failed (non-convex), 2 a row is not an inequality
+    int *flags;        // OR over plants: 1 setup failed (non-convex), 2 a row is not an inequality,
+                       // 4 the Jacobi eigen-solve hit its sweep cap (inaccurate basis)
 };
 
 // Arguments of the ADMM kernel (one QP per lane).

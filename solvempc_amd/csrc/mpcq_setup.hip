@@ -186,6 +186,7 @@ __global__ __launch_bounds__(64) void setup_kernel(SetupArgs a)
     __syncthreads();
 
     // ---- 3d. cyclic Jacobi: C = V diag(lambda) V'
+    bool converged = false;
     for (int sweep = 0; sweep < 60; sweep++) {
         if (t == 0) {
             double off = 0.0, dia = 0.0;
@@ -197,7 +198,7 @@ __global__ __launch_bounds__(64) void setup_kernel(SetupArgs a)
             sh[2] = (off <= 1e-32 * dia || off < 1e-300) ? 1.0 : 0.0;
         }
         __syncthreads();
-        if (sh[2] != 0.0) break;
+        if (sh[2] != 0.0) { converged = true; break; }
         for (int pp = 0; pp < n - 1; pp++)
             for (int qq = pp + 1; qq < n; qq++) {
                 const double apq = C[pp * n + qq];
@@ -286,6 +287,7 @@ __global__ __launch_bounds__(64) void setup_kernel(SetupArgs a)
     if (t == 0) {
         a.status[p] = fail ? kNonCvx : 0;
         if (fail) atomicOr(a.flags, 1);
+        if (!converged) atomicOr(a.flags, 4);  // sweep cap hit: (lambda, W) would be inaccurate
     }
 }
 

@@ -258,6 +258,7 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
         while (bu0 < np && bb >= np - bu0) { bb -= np - bu0; bu0++; }
         bv0 = bu0 + bb;
     }
+    bool converged = ne <= 1;
     for (int sweep = 0; sweep < 60 && ne > 1; sweep++) {
         double off = 0.0, dia = 0.0;
         for (int e = t; e < n * n; e += 64) {
@@ -268,7 +269,7 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
         off = wave_sum(off);
         dia = wave_sum(dia);
         if (a.prof && t == 0) a.prof[(size_t)pl * 16 + 15] = sweep;
-        if (off <= 1e-32 * dia || off < 1e-300) break;
+        if (off <= 1e-32 * dia || off < 1e-300) { converged = true; break; }
         for (int r = 0; r < ne - 1; r++) {
             if (t < np) {
                 int pp, qq;
@@ -394,6 +395,7 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
     if (t == 0) {
         a.status[pl] = fail ? kNonCvx : 0;
         if (fail) atomicOr(a.flags, 1);
+        if (!converged) atomicOr(a.flags, 4);  // sweep cap hit: (lambda, W) would be inaccurate
     }
 }
 

@@ -472,3 +472,51 @@ def test_per_plant_device_pipeline(plant):
         assert st[b] == st_o and it[b] == r.info().iter, b
         u_ref = U[b] + (r.x()[0] if st_o == sm.SOLVED else 0.0)
         assert abs(Ug[b] - u_ref) < 1e-9, b
+
+
+def test_stream_graph_recaptured_after_replant(plant):
+    """The hipGraph of mpcq_mpc_run_device bakes in operator/plant buffers and kernel-variant flags:
+    re-planting the context (mpcq_mpc_setup_plants_device with another nx, which reallocates those
+    buffers, and mpcq_mpc_set_plant) must invalidate it.  Each phase is checked against the oracle's
+    controllerStep driven by the device's X."""
+    import torch
+
+    N, B, steps = 20, 32, 3
+    dev = torch.device("cuda:0")
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64), device=dev)  # noqa: E731
+    s = sm.BatchSolver(N, 2 * N, B, n_plants=B)
+    st = torch.cuda.Stream()
+    Xbuf = torch.zeros(B * 4, dtype=torch.float64, device=dev)  # the same X/U pointers in every phase:
+    Ud = torch.zeros(B, dtype=torch.float64, device=dev)        # only the generation tells the graphs apart
+    for phase, nx in enumerate((4, 3, 4)):
+        pl = dict(plant, Ad=plant["Ad"][:nx, :nx].copy(), Bd=plant["Bd"][:nx].copy(), Cd=plant["Cd"][:nx].copy(),
+                  K=plant["K"][:nx].copy())
+        Ad = np.tile(pl["Ad"], (B, 1, 1))
+        Bd = np.tile(pl["Bd"], (B, 1))
+        keep = [t(Ad), t(Bd), t(np.tile(pl["Cd"], (B, 1))), t(np.tile(pl["K"], (B, 1))), t(np.full(B, pl["Q"])),
+                t(np.full(B, pl["R"])), t(np.full(B, pl["RD"]))]
+        torch.cuda.synchronize()
+        s.mpc_setup_plants_device(nx, 10, *[k.data_ptr() for k in keep], st.cuda_stream)
+        st.synchronize()
+        s.mpc_set_plant(Ad, Bd)
+        X, U = workload.mpc_states(50 + phase, 0, B)
+        X = X[:, :nx].copy()
+        Xd = Xbuf[:B * nx]
+        Xd.copy_(t(X.reshape(-1)))
+        Ud.copy_(t(U))
+        torch.cuda.synchronize()
+        ops = oracle.condense(pl, N)
+        l = np.full(2 * N, LMIN)
+        refs = [oracle.Solver(ops["P"], np.zeros(N), ops["A"], l, ops["W0"]) for _ in range(B)]
+        Xk, Uk = X.copy(), U.copy()
+        for k in range(steps):
+            with torch.cuda.stream(st):
+                s.mpc_run_device(Xd.data_ptr(), Ud.data_ptr(), 0.0, 1, 9, 0, k, 1e-2, st.cuda_stream)
+            st.synchronize()
+            for b, r in enumerate(refs):
+                assert r.update_gradient(oracle.gradient(ops, Xk[b], Uk[b]))
+                assert r.update_upper_bound(oracle.upper_bound(ops, Xk[b], Uk[b]))
+                if r.solve() == oracle.SOLVED:
+                    Uk[b] += r.x()[0]
+            np.testing.assert_allclose(Ud.cpu().numpy(), Uk, rtol=0, atol=1e-9, err_msg=f"phase {phase} step {k}")
+            Xk = Xd.cpu().numpy().reshape(B, nx).copy()
