@@ -228,7 +228,10 @@ def main():
     status, iters, _ = solver.info()
     qps_per_step = B * (a.ctrl_steps if stream_mode else 1)
     # stream: iterations of the last control step stand for every step (estimate, see "flops_note")
-    flops = float(workload.flops_per_qp(N, 2 * N, 4, iters).sum()) * (a.ctrl_steps if stream_mode else 1)
+    kind, paired = solver.path()
+    reps = a.ctrl_steps if stream_mode else 1
+    flops = float(workload.flops_per_qp(N, 2 * N, 4, iters, paired=paired).sum()) * reps
+    flops_dense = float(workload.flops_per_qp(N, 2 * N, 4, iters).sum()) * reps
     achieved = flops / (kern_ms * 1e-3) / 1e12
     if perplant:
         setup_flops = B * workload.flops_plant_setup(N, 2 * N)
@@ -263,10 +266,15 @@ def main():
                     "batch_per_gpu": B, "horizon": N, "ctrl_steps": a.ctrl_steps, "parallelism": f"dp{world}"}),
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS[a.dtype], "unit": "TFLOP/s",
                      "frac": achieved / PEAK_TFLOPS[a.dtype], "traffic": traffic_per_solve(a.dtype, B, N),
-                     "kernel": "admm_tile_kernel (all phase launches of one solve)",
+                     "kernel": f"admm_{kind}_kernel{' (paired loop)' if paired else ''} (all phase launches of one solve)",
                      "kernel_ms": kern_ms, "flops_per_step": flops,
+                     "dense_equivalent": {"flops_per_step": flops_dense,
+                                          "achieved": flops_dense / (kern_ms * 1e-3) / 1e12,
+                                          "frac": flops_dense / (kern_ms * 1e-3) / 1e12 / PEAK_TFLOPS[a.dtype]},
                      "flops_note": "algorithmic: sum over QPs of iters*F_iter + checks*F_check + front end "
                                    "(SURVEY §8d, DESIGN §4.1), actual per-QP iteration counts"
+                                   + ("; F_iter counts the m/2-row products the paired loop performs "
+                                      "(dense_equivalent: the dense 4nm count)" if paired else "")
                                    + ("; stream: last control step's counts x ctrl_steps (estimate)" if stream_mode else "")},
         "iters": {"mean": float(iters.mean()), "max": int(iters.max()), "solved_frac": solved},
     }

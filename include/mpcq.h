@@ -126,6 +126,15 @@ int mpcq_get_dual(mpcq_ctx *ctx, double *y);                /* batch*m */
 int mpcq_get_info(mpcq_ctx *ctx, int *status, int *iter, double *rho); /* each batch, may be NULL */
 int mpcq_get_scaling(mpcq_ctx *ctx, double *D, double *E, double *c); /* plant 0: n, m, 1 */
 
+/* Device path the next solve takes (no OSQP counterpart; for benchmarks and tests):
+ * *kind = MPCQ_PATH_TILE (shared plant, MFMA tile kernel + one-QP-per-wave tail), MPCQ_PATH_WAVE
+ * (one QP per wave) or MPCQ_PATH_LANE (one QP per lane); *paired = 1 when the tile kernel runs its
+ * paired loop (rows n + j of A are the negated rows j: the condensed-MPC constraint matrix). */
+#define MPCQ_PATH_TILE 0
+#define MPCQ_PATH_WAVE 1
+#define MPCQ_PATH_LANE 2
+int mpcq_get_path(mpcq_ctx *ctx, int *kind, int *paired);
+
 int mpcq_device_view_get(mpcq_ctx *ctx, mpcq_device_view *view);
 
 /* ---- condensed-MPC front end: ModelPredictiveControlAPI::controllerStep, batched ------------

@@ -149,6 +149,12 @@ class BatchSolver:
         _capi.check(lib().mpcq_get_scaling(self._ctx, _dp(D), _dp(E), C.byref(c)), "mpcq_get_scaling")
         return D, E, c.value
 
+    def path(self) -> tuple[str, bool]:
+        """(kernel family of the next solve: "tile" / "wave" / "lane", paired tile loop)."""
+        k, p = C.c_int(), C.c_int()
+        _capi.check(lib().mpcq_get_path(self._ctx, C.byref(k), C.byref(p)), "mpcq_get_path")
+        return ("tile", "wave", "lane")[k.value], bool(p.value)
+
     def device_view(self) -> dict:
         v = _capi.DeviceView()
         _capi.check(lib().mpcq_device_view_get(self._ctx, C.byref(v)), "mpcq_device_view_get")

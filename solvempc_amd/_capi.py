@@ -18,7 +18,7 @@ EXPORTS = (
     "mpcq_cold_start", "mpcq_reset", "mpcq_solve", "mpcq_get_solution", "mpcq_get_dual", "mpcq_get_info",
     "mpcq_get_scaling", "mpcq_device_view_get", "mpcq_mpc_set_operators", "mpcq_mpc_step_device",
     "mpcq_mpc_step", "mpcq_mpc_set_plant", "mpcq_mpc_simulate_device", "mpcq_mpc_run_device",
-    "mpcq_condense", "mpcq_mpc_setup_plants_device", "mpcq_last_error",
+    "mpcq_condense", "mpcq_mpc_setup_plants_device", "mpcq_last_error", "mpcq_get_path",
 )
 
 
@@ -84,6 +84,7 @@ def lib() -> C.CDLL:
         "mpcq_get_dual": (C.c_int, [vp, dp]),
         "mpcq_get_info": (C.c_int, [vp, ip, ip, dp]),
         "mpcq_get_scaling": (C.c_int, [vp, dp, dp, dp]),
+        "mpcq_get_path": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "mpcq_device_view_get": (C.c_int, [vp, C.POINTER(DeviceView)]),
         "mpcq_mpc_set_operators": (C.c_int, [vp, C.c_int, dp, dp, dp, dp, dp, dp]),
         "mpcq_mpc_step_device": (C.c_int, [vp, vp, vp, C.c_double, vp]),

@@ -48,11 +48,13 @@ struct mpcq_ctx {
     int nc = 0, mc = 0;
     size_t ops_stride = 0;
     bool setup_done = false, all_ineq = true, mpc_ready = false, lower_free = false, fresh = false;
+    bool paired = false;  // shared plant of the condensed-MPC shape (tile kernel's paired loop)
     // tile (MFMA) path: shared plant with a compiled (KN, KM) shape
     bool tile = false;
     int KN = 0, KM = 0;
     void *d_img = nullptr;
     int *d_list = nullptr, *d_counts = nullptr, *d_itstate = nullptr;
+    long long *d_stamps = nullptr;  // debug (MPCQ_TILE_STAMPS)
     hipStream_t last = nullptr;
     int nx = 0;
     // setup
@@ -143,6 +145,7 @@ mpcq::AdmmArgs<T> make_args(mpcq_ctx *c)
     const int ct = c->set.check_termination;
     a.adaptive_interval = c->set.adaptive_rho_interval ? c->set.adaptive_rho_interval : (ct ? 4 * ct : 100);
     a.all_ineq = c->all_ineq;
+    a.paired = c->paired && c->tile && std::strcmp(std::getenv("MPCQ_PAIRED") ? std::getenv("MPCQ_PAIRED") : "1", "0") != 0;
     a.lower_free = c->lower_free;
     a.q = c->d_q;
     a.u = c->d_u;
@@ -351,7 +354,7 @@ int mpcq_destroy(mpcq_ctx *c)
                     c->d_setup_status, c->d_q, c->d_u, c->d_l, c->d_x, c->d_y, c->d_rho, c->d_status, c->d_iter,
                     c->d_xs, c->d_zs, c->d_ys, c->d_rhos, c->d_snx, c->d_sny, c->d_Fx, c->d_Fu, c->d_Fr,
                     c->d_Sbar, c->d_Ku, c->d_W0, c->d_X, c->d_U, c->d_img, c->d_list, c->d_counts,
-                    c->d_itstate, c->d_Ad, c->d_Bd, c->d_step, c->d_flags};
+                    c->d_itstate, c->d_Ad, c->d_Bd, c->d_step, c->d_flags, c->d_stamps};
     if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
     if (c->graph) (void)hipGraphDestroy(c->graph);
     for (void *p : ptrs)
@@ -454,6 +457,11 @@ int mpcq_setup(mpcq_ctx *c, const double *P, const double *q0, const double *A, 
     for (size_t i = 0; i < Pn * m; i++)
         if (l0[i] > u0[i]) return fail(MPCQ_ERR_BOUNDS, "lower bound above upper bound (osqp validate_data)");
     c->setup_done = false;
+    // rows n + j of A are the negated rows j (the reference's Gbar = [K0 L; -K0 L],
+    // ModelPredictiveControlAPI.cpp:332-347), checked bit for bit: the tile kernel's paired loop
+    c->paired = Pn == 1 && m == 2 * n && n % 4 == 0;
+    for (size_t i = 0; c->paired && i < n * n; i++)
+        if (!(A[n * n + i] == -A[i])) c->paired = false;
     hipStream_t s = c->last;
     if ((rc = h2d(c->d_P, P, 8 * Pn * n * n, s)) || (rc = h2d(c->d_q0, q0, 8 * Pn * n, s)) ||
         (rc = h2d(c->d_A, A, 8 * Pn * m * n, s)) || (rc = h2d(c->d_l0, l0, 8 * Pn * m, s)) ||
@@ -600,8 +608,16 @@ static int launch_args(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s)
     // Small batches (under 512 tile waves) are latency-bound: one QP per wave from the start.
     const bool small = B < 8192 && std::strcmp(env_kernel(), "tile") != 0;
     const int tail_from = (all_wave || small) ? 0 : (te ? std::atoi(te) : 3);
+    int np_run = 0;
 
+    // debug hook: per-wave stage stamps of every phase launch, written to $MPCQ_TILE_STAMPS after the solve
+    const char *stp = std::getenv("MPCQ_TILE_STAMPS");
+    const size_t waves = (size_t)(B + 15) / 16 + 4;
+    if (stp && *stp && !c->d_stamps && hipMalloc((void **)&c->d_stamps, 8 * 8 * waves * kMaxPhases) != hipSuccess)
+        return -2;
+    if (stp && *stp && hipMemsetAsync(c->d_stamps, 0, 8 * 8 * waves * kMaxPhases, s) != hipSuccess) return -2;
     for (int p = 0; p < np; p++) {
+        a.stamps = (stp && *stp) ? c->d_stamps + (size_t)p * 8 * waves : nullptr;
         a.img = (const T *)c->d_img;
         a.list_in = p ? c->d_list + (size_t)(p % 2) * B : nullptr;
         a.count_in = p ? c->d_counts + (p - 1) : nullptr;
@@ -617,12 +633,26 @@ static int launch_args(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s)
             a.stop_iter = c->set.max_iter;
             rc = wave_launch<T>(c, a, p == 0 ? B : std::min(B, 2048), s);
             if (rc) return rc;
+            np_run = p;
             break;
         } else
             rc = std::is_same<T, float>::value
                      ? mpcq_internal_tile_launch_f32((const mpcq::AdmmArgs<float> *)&a, c->KN, c->KM, s)
                      : mpcq_internal_tile_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->KN, c->KM, s);
         if (rc) return rc;
+        np_run = p + 1;
+    }
+    if (stp && *stp) {
+        std::vector<long long> h(8 * waves * kMaxPhases);
+        if (hipMemcpyAsync(h.data(), c->d_stamps, 8 * h.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -2;
+        if (FILE *f = std::fopen(stp, "wb")) {
+            const long long hdr[2] = {(long long)np_run, (long long)waves};
+            std::fwrite(hdr, 8, 2, f);
+            std::fwrite(h.data(), 8, 8 * waves * np_run, f);
+            std::fclose(f);
+        }
     }
     return 0;
 }
@@ -707,6 +737,21 @@ int mpcq_get_scaling(mpcq_ctx *c, double *D, double *E, double *cc)
     if (D) std::copy(c->hD.begin(), c->hD.end(), D);
     if (E) std::copy(c->hE.begin(), c->hE.end(), E);
     if (cc) *cc = c->hc;
+    return MPCQ_OK;
+}
+
+int mpcq_get_path(mpcq_ctx *c, int *kind, int *paired)
+{
+    if (!c) return fail(MPCQ_ERR_ARG, "null context");
+    const char *k = env_kernel();
+    int kd;
+    if (c->tile && std::strcmp(k, "lane") != 0) kd = std::strcmp(k, "wave") == 0 ? MPCQ_PATH_WAVE : MPCQ_PATH_TILE;
+    else kd = (std::strcmp(k, "lane") == 0 || c->dims.n > 32 || c->dims.m > 64) ? MPCQ_PATH_LANE : MPCQ_PATH_WAVE;
+    if (kind) *kind = kd;
+    if (paired) {
+        const char *pe = std::getenv("MPCQ_PAIRED");
+        *paired = kd == MPCQ_PATH_TILE && c->paired && c->all_ineq && c->lower_free && !(pe && !std::strcmp(pe, "0"));
+    }
     return MPCQ_OK;
 }
 

@@ -121,6 +121,7 @@ struct AdmmArgs {
     SolverSettings st;
     int adaptive_interval;      // resolved (0 -> 4*check_termination)
     int all_ineq;               // every row of every plant is an inequality (constr_type 0)
+    int paired;                 // shared plant with m = 2n, n % 4 == 0, A rows n + j == -rows j (tile kernel)
     int lower_free;             // every l^ of every QP is below -OSQP_INFTY*MIN_SCALING
     // per-QP inputs (fp64, QP-major as in the C ABI)
     const double *q, *u, *l;    // batch*n, batch*m, batch*m (l may be a single shared m-vector)
@@ -148,6 +149,7 @@ struct AdmmArgs {
     int *it_state;              // [batch] iterations done so far in this solve
     int stop_iter;              // phase boundary (multiple of check_termination, or max_iter)
     int resume;                 // 1: phase >= 2 (state, rho and iteration count come from the buffers)
+    long long *stamps;          // debug (MPCQ_TILE_STAMPS): [wave][8] s_memtime / s_memrealtime stamps, or null
 };
 
 // MFMA operand images of one shared plant for the tile kernel (mpcq_tile.h).  A vector of length

@@ -52,6 +52,20 @@ template <typename T> __device__ __forceinline__ T tt_max(T a, T b) { return a >
 template <typename T> __device__ __forceinline__ T tt_min(T a, T b) { return a < b ? a : b; }
 // max(m, |x|) for the infinity norms (one v_max with an |.| source modifier; equals OSQP's
 // c_max(m, c_absval(x)) for every non-NaN x).
+// min for the projection onto u without LLVM's NaN canonicalisation of the operands (a v_max x, x
+// per element per iteration): the hardware v_min returns the non-NaN operand, as fmin does.
+__device__ __forceinline__ float vmin(float a, float b)
+{
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double vmin(double a, double b)
+{
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 template <typename T> __device__ __forceinline__ T nrm(T m, T x) { return __builtin_fmax(m, __builtin_fabs(x)); }
 
 // Reductions over the 4 lanes (groups) of one QP column (lanes c, c+16, c+32, c+48) with the gfx950
@@ -190,11 +204,64 @@ __device__ __forceinline__ void tile_mv_g(const T *__restrict__ im, const T (&x)
             for (int r = 0; r < 4; r++) y[gi][4 * t + r] = acc[gi][t][r];
 }
 
+// Products with the A operand held in VGPRs (one f32/f64 register per lane per tile and k-step: the
+// 16x16x4 A fragment, lane l = A[16 t + arow(l & 15)][4 s + (l >> 4)]), for the paired hot loop:
+// y = init + M1 x1 (+ M2 x2), the NTO x G accumulator chains interleaved k-step by k-step.
+template <typename T, int G, int NTO, int KS, int XN, bool TWO, int XN2>
+__device__ __forceinline__ void reg_mv(const T (&m1)[NTO][KS], const T (&x1)[G][XN], const T (&m2)[NTO][KS],
+                                       const T (&x2)[G][XN2], T (&y)[G][4 * NTO], const T (*init)[4 * NTO])
+{
+    using A = typename Mf<T>::acc;
+    A acc[G][NTO];
+#pragma unroll
+    for (int gi = 0; gi < G; gi++)
+#pragma unroll
+        for (int t = 0; t < NTO; t++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) acc[gi][t][r] = init ? init[gi][4 * t + r] : T(0);
+#pragma unroll
+    for (int s = 0; s < KS; s++)
+#pragma unroll
+        for (int t = 0; t < NTO; t++)
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) acc[gi][t] = Mf<T>::mma(m1[t][s], x1[gi][s], acc[gi][t]);
+    if constexpr (TWO) {
+#pragma unroll
+        for (int s = 0; s < KS; s++)
+#pragma unroll
+            for (int t = 0; t < NTO; t++)
+#pragma unroll
+                for (int gi = 0; gi < G; gi++) acc[gi][t] = Mf<T>::mma(m2[t][s], x2[gi][s], acc[gi][t]);
+    }
+#pragma unroll
+    for (int gi = 0; gi < G; gi++)
+#pragma unroll
+        for (int t = 0; t < NTO; t++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) y[gi][4 * t + r] = acc[gi][t][r];
+}
+
 // G: 16-QP groups per wave; OCC: waves per SIMD the register allocation is held to (256-thread
 // workgroups, so one workgroup carries 64 G QPs).
-template <typename T, int KN, int KM, bool ALL_INEQ, bool LFREE, int G, int OCC>
+// PAIRED (the condensed-MPC shape, m = 2n, n % 4 == 0, rows n + j = -rows j of A, all inequality
+// rows, l = -inf; ModelPredictiveControlAPI.cpp:326-347 builds A = [K0 L; -K0 L]): Ruiz gives rows
+// j and n + j the same E, so B = A^ W has B_{n+j} = -B_j exactly.  The hot loop then computes
+// z~ for the top half only (z~_{n+j} = -z~_j) and B' w as B~' (w_top - w_bot), and keeps its three
+// operators S, B~', B~ (3 NT KN registers) in VGPRs: no LDS traffic between check iterations.
+// Element 4 s + g of a half-m vector pairs register s with register s + KN (same lane).
+// Debug hook (MPCQ_TILE_STAMPS): per-wave shader-clock stamps at the stage boundaries of a launch:
+// 0 entry, 1 images in LDS, 2 loop entry, 3 phase-boundary save, 4 exit, 5 iteration at exit,
+// 6 / 7 s_memrealtime (100 MHz) at entry / exit.
+#define MPCQ_TSTAMP(k, v)                                                                                  \
+    do {                                                                                                   \
+        if (a.stamps && (threadIdx.x & 63) == 0) a.stamps[(size_t)(blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (k)] = (v); \
+    } while (0)
+template <typename T, int KN, int KM, bool ALL_INEQ, bool LFREE, int G, int OCC, bool PAIRED = false>
 __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
 {
+    MPCQ_TSTAMP(0, (long long)__builtin_amdgcn_s_memtime());
+    MPCQ_TSTAMP(6, (long long)__builtin_amdgcn_s_memrealtime());
+    static_assert(!PAIRED || (KM == 2 * KN && ALL_INEQ && LFREE), "paired loop: m = 2n, inequality rows, l free");
     constexpr int VEC = 16 / sizeof(T);
     constexpr TileLayout L = TileLayout::make(KN, KM, VEC);
     constexpr int NT = L.NT, MT = L.MT, KNP = L.KNP, KMP = L.KMP;
@@ -217,18 +284,68 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
         s_Einv[i] = a.ops.Einv[i];
     }
 
-    // ---- plant images -> LDS (16 B per thread per step)
+    // ---- plant images -> LDS (16 B per thread per step; every load issued before the stores)
     {
         typedef T vec __attribute__((ext_vector_type(VEC)));
         const vec *src = (const vec *)a.img;
         vec *dst = (vec *)img;
-        for (int i = threadIdx.x; i < (int)(L.total / VEC); i += 256) dst[i] = src[i];
+        constexpr int NV = (int)(L.total / VEC), PER = (NV + 255) / 256;
+        vec buf[PER];
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const int i = threadIdx.x + 256 * k;
+            buf[k] = src[i < NV ? i : 0];
+        }
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const int i = threadIdx.x + 256 * k;
+            if (i < NV) dst[i] = buf[k];
+        }
+    }
+    // ---- MPC front-end operators of the plant (setF :372-375, setUpperBound :360-369) -> LDS, fp64:
+    // Fx, Sbar rows padded to 8 columns; frr = Fr (xref 1) summed per row in the reference's order.
+    constexpr int FE_FX = 0, FE_FU = 8 * NCP, FE_FR = 9 * NCP, FE_SB = 10 * NCP, FE_KU = 10 * NCP + 8 * MCP,
+                  FE_W0 = 10 * NCP + 9 * MCP, FE_E = 10 * NCP + 10 * MCP, FE_D = 10 * NCP + 11 * MCP,
+                  FE_TOT = 11 * NCP + 11 * MCP;
+    __shared__ double fe[FE_TOT];
+    {
+        const int n = a.n, m = a.m, nx = a.mpc ? a.nx : 0;
+        for (int i = threadIdx.x; i < MCP; i += 256) fe[FE_E + i] = i < m ? (double)a.ops.E[i] : 0.0;
+        for (int i = threadIdx.x; i < NCP; i += 256) fe[FE_D + i] = i < n ? (double)a.ops.D[i] : 0.0;
+        if (a.mpc) {
+            for (int i = threadIdx.x; i < 8 * NCP; i += 256) {
+                const int v = i >> 3, t = i & 7;
+                fe[FE_FX + i] = (v < n && t < nx) ? a.Fx[(size_t)v * nx + t] : 0.0;
+            }
+            for (int i = threadIdx.x; i < 8 * MCP; i += 256) {
+                const int v = i >> 3, t = i & 7;
+                fe[FE_SB + i] = (v < m && t < nx) ? a.Sbar[(size_t)v * nx + t] : 0.0;
+            }
+            for (int i = threadIdx.x; i < NCP; i += 256) fe[FE_FU + i] = i < n ? a.Fu[i] : 0.0;
+            for (int i = threadIdx.x; i < MCP; i += 256) {
+                fe[FE_KU + i] = i < m ? a.Ku[i] : 0.0;
+                fe[FE_W0 + i] = i < m ? a.W0[i] : 0.0;
+            }
+            if (threadIdx.x < n) {  // Fr ref, ref = xref 1 (updateRef :378-380): row sums in order t = 0..n-1
+                const int v = threadIdx.x;
+                double fr[NCP];
+#pragma unroll
+                for (int t = 0; t < NCP; t++) fr[t] = a.Fr[(size_t)v * n + (t < n ? t : 0)];
+                double s2 = 0.0;
+#pragma unroll
+                for (int t = 0; t < NCP; t++)
+                    if (t < n) s2 += fr[t] * a.xref;
+                fe[FE_FR + v] = s2;
+            }
+        }
     }
     __syncthreads();  // the only barrier: waves are independent from here on
+    MPCQ_TSTAMP(1, (long long)__builtin_amdgcn_s_memtime());
 
     const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
     const int wave_slot = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 * G;
     if (wave_slot >= count) return;
+    constexpr int KNR = PAIRED ? KN : 1, NTR = PAIRED ? NT : 1;
     bool valid[G];
     int b_[G];
 #pragma unroll
@@ -245,72 +362,92 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
     const bool scaled_term = st.scaled_termination != 0;
     const double c64 = (double)op.cs[0];
 
-    // ---- per-QP data (element v = 4 s + g of this lane's QP column), per group
-    T qh[G][NS];  // q^ = c D q (osqp_update_lin_cost), kept for the dual residual
+    // ---- per-QP data (element v = 4 s + g of this lane's QP column), per group.  Every global load
+    // of a group is issued (index clamped into the row, not branched) before any of it is used.
+    T qh[G][NS];  // q^ = c D q (osqp_update_lin_cost): prologue only; the checks re-read q (load_qh)
     T uh[G][MS], lh[G][LFREE ? 1 : MS];
     T rs[ALL_INEQ ? 1 : MS];
     int status[G];
 #pragma unroll
     for (int gi = 0; gi < G; gi++) {
         const int b = b_[gi];
-        double Xv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        double Uv = 0.0;
-        if (a.mpc) {
+        double qk[KN], up[KM], lo[LFREE ? 1 : KM];
+        if (a.mpc) {  // setF (:372-375) q = Fx X + Fu U + Fr ref;  (:93-99) u = W0 + Sbar X + Ku U
+            double Xv[8];
+            const int nx = a.nx;
+#pragma unroll
+            for (int t = 0; t < 8; t++) Xv[t] = a.X[(size_t)b * nx + (t < nx ? t : 0)];
+            const double Uv = a.U[b];
 #pragma unroll
             for (int t = 0; t < 8; t++)
-                if (t < a.nx) Xv[t] = a.X[(size_t)b * a.nx + t];
-            Uv = a.U[b];
+                if (t >= nx) Xv[t] = 0.0;
+#pragma unroll
+            for (int s = 0; s < KN; s++) {
+                const int v = 4 * s + g;  // < NCP: padded rows of fe are zero
+                double s0 = 0.0;
+#pragma unroll
+                for (int t = 0; t < 8; t++)
+                    if (t < nx) s0 += fe[FE_FX + 8 * v + t] * Xv[t];
+                const double s1 = fe[FE_FU + v] * Uv;
+                qk[s] = s0 + s1 + fe[FE_FR + v];
+                if (valid[gi] && v < n) a.q_out[(size_t)b * n + v] = qk[s];
+            }
+#pragma unroll
+            for (int s = 0; s < KM; s++) {
+                const int v = 4 * s + g;
+                double sx = 0.0;
+#pragma unroll
+                for (int t = 0; t < 8; t++)
+                    if (t < nx) sx += fe[FE_SB + 8 * v + t] * Xv[t];
+                up[s] = fe[FE_W0 + v] + sx + fe[FE_KU + v] * Uv;
+                if (valid[gi] && v < m) a.u_out[(size_t)b * m + v] = up[s];
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < KN; s++) {
+                const int v = 4 * s + g;
+                qk[s] = a.q[(size_t)b * n + (v < n ? v : 0)];
+            }
+#pragma unroll
+            for (int s = 0; s < KM; s++) {
+                const int v = 4 * s + g;
+                up[s] = a.u[(size_t)b * m + (v < m ? v : 0)];
+            }
+        }
+        if constexpr (!LFREE) {
+#pragma unroll
+            for (int s = 0; s < KM; s++) {
+                const int v = 4 * s + g;
+                lo[s] = a.l[(a.l_shared ? 0 : (size_t)b * m) + (v < m ? v : 0)];
+            }
         }
 #pragma unroll
         for (int s = 0; s < NS; s++) {
             const int v = 4 * s + g;
-            double qk = 0.0;
-            if (s < KN && v < n) {
-                if (a.mpc) {  // setF (:372-375): q = Fx X + Fu U + Fr ref
-                    const double *fx = a.Fx + (size_t)v * a.nx;
-                    const double *fr = a.Fr + (size_t)v * n;
-                    double s0 = 0.0, s2 = 0.0;
-#pragma unroll
-                    for (int t = 0; t < 8; t++)
-                        if (t < a.nx) s0 += fx[t] * Xv[t];
-                    const double s1 = a.Fu[v] * Uv;
-                    for (int t = 0; t < n; t++) s2 += fr[t] * a.xref;
-                    qk = s0 + s1 + s2;
-                    if (valid[gi]) a.q_out[(size_t)b * n + v] = qk;
-                } else {
-                    qk = a.q[(size_t)b * n + v];
-                }
-            }
-            qh[gi][s] = s < KN ? (T)((qk * (double)op.D[s < KN ? v : 0]) * c64) : T(0);
+            qh[gi][s] = (s < KN && v < n) ? (T)((qk[s < KN ? s : 0] * fe[FE_D + v]) * c64) : T(0);
         }
         int bad = 0, tchg = 0;
 #pragma unroll
         for (int s = 0; s < MS; s++) {
             const int v = 4 * s + g;
-            double up = kInfty, lo = -kInfty;
+            double uu = kInfty, ll = -kInfty;
             if (s < KM && v < m) {
-                if (a.mpc) {  // setUpperBound (:360-369) + :99: u = W0 + Sbar X + Ku U
-                    const double *sb = a.Sbar + (size_t)v * a.nx;
-                    double sx = 0.0;
-#pragma unroll
-                    for (int t = 0; t < 8; t++)
-                        if (t < a.nx) sx += sb[t] * Xv[t];
-                    up = a.W0[v] + sx + a.Ku[v] * Uv;
-                    if (valid[gi]) a.u_out[(size_t)b * m + v] = up;
-                } else {
-                    up = a.u[(size_t)b * m + v];
+                const double e = fe[FE_E + v];  // osqp_update_bounds: u^ = E u, l^ = E l
+                uu = up[s] * e;
+                if constexpr (!LFREE) ll = lo[s] * e;
+                if (!a.resume) {  // a resumed phase's QPs passed these checks in phase 0
+                    if (uu < ll) bad = 1;
+                    if constexpr (ALL_INEQ && LFREE) {
+                        if (uu > kInfty * kMinScaling) tchg = 1;  // a free row: not the setup's type
+                    } else {
+                        const int ty = (ll < -kInfty * kMinScaling && uu > kInfty * kMinScaling) ? -1
+                                                                                             : (uu - ll < kRhoTol ? 1 : 0);
+                        if (ty != ctype[v]) tchg = 1;
+                    }
                 }
-                lo = a.l[(a.l_shared ? 0 : (size_t)b * m) + v];
-                const double e = (double)op.E[v];  // osqp_update_bounds: u^ = E u, l^ = E l
-                up *= e;
-                lo *= e;
-                if (up < lo) bad = 1;
-                const int ty = (lo < -kInfty * kMinScaling && up > kInfty * kMinScaling) ? -1 : (up - lo < kRhoTol ? 1 : 0);
-                if (ty != ctype[v]) tchg = 1;
-                if (LFREE && !((T)lo < T(-kInfty * kMinScaling))) tchg = 1;
             }
-            uh[gi][s] = (T)up;
-            if (!LFREE) lh[gi][s] = (T)lo;
+            uh[gi][s] = (T)uu;
+            if (!LFREE) lh[gi][s] = (T)ll;
             if (!ALL_INEQ && gi == 0) rs[s] = (s < KM && v < m) ? (ctype[v] == -1 ? T(-1) : op.rscale[v]) : T(1);
         }
         bad = col_or(bad);
@@ -437,7 +574,133 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
     const int stop = a.stop_iter;
     int next_check = ct ? (it / ct + 1) * ct : -1;  // uniform; no integer division in the loop
     int next_adapt = ai ? (it / ai + 1) * ai : -1;
+    T dx[G][NS], dy[G][MS];
+    // paired loop: operators S, B~', B~ from the LDS images into VGPRs (A-fragment per tile, k-step)
+    auto load_regs = [&](T (&rS)[NTR][KNR], T (&rBt)[NTR][KNR], T (&rB)[NTR][KNR]) {
+        const T *im = fresh_ptr((const T *)img);
+#pragma unroll
+        for (int t = 0; t < NTR; t++)
+#pragma unroll
+            for (int k = 0; k < KNR; k++) {
+                rS[t][k] = im[L.S + TileLayout::at(KNP, VEC, t, k, lane)];
+                rBt[t][k] = im[L.Bt + TileLayout::at(KMP, VEC, t, k, lane)];
+                rB[t][k] = im[L.B + TileLayout::at(KNP, VEC, t, k, lane)];
+            }
+    };
+    // one paired ADMM iteration (see the PAIRED note above the kernel)
+    auto piter = [&](auto with_delta, const T (&rS)[NTR][KNR], const T (&rBt)[NTR][KNR], const T (&rB)[NTR][KNR]) {
+        constexpr bool DELTA = decltype(with_delta)::value;
+        if constexpr (PAIRED) {
+            // xi = -g + S x' + B~' (w_top - w_bot),  w = rho z - y
+            T wt[G][KNR];
+#pragma unroll
+            for (int gi = 0; gi < G; gi++)
+#pragma unroll
+                for (int s = 0; s < KN; s++)
+                    wt[gi][s] = tt_fma(rho[gi], z[gi][s], -y[gi][s]) - tt_fma(rho[gi], z[gi][s + KN], -y[gi][s + KN]);
+            T xi[G][NS];
+            reg_mv<T, G, NT, KN, NS, true>(rS, xs, rBt, wt, xi, gv);
+#pragma unroll
+            for (int gi = 0; gi < G; gi++)
+#pragma unroll
+                for (int s = 0; s < KN; s++) {
+                    xi[gi][s] = xi[gi][s] * dk[gi][s];
+                    const T xn = tt_fma(alpha, xi[gi][s], oma * xs[gi][s]);
+                    if (DELTA) dx[gi][s] = xn - xs[gi][s];
+                    xs[gi][s] = xn;
+                }
+            // z~_top = B~ eta (z~_bot = -z~_top) ; relaxation ; projection ; dual update
+            T zt[G][NS];
+            reg_mv<T, G, NT, KN, NS, false>(rB, xi, rB, wt, zt, nullptr);
+#pragma unroll
+            for (int gi = 0; gi < G; gi++)
+#pragma unroll
+                for (int s = 0; s < KM; s++) {
+                    const T rj = rho[gi], rij = rinv[gi];
+                    const T zts = s < KN ? zt[gi][s] : -zt[gi][s - KN];
+                    const T v = tt_fma(alpha, zts, oma * z[gi][s]);
+                    T zn = tt_fma(rij, y[gi][s], v);
+                    zn = __builtin_fmin(zn, uh[gi][s]);
+                    if (DELTA) dy[gi][s] = rj * (v - zn);
+                    y[gi][s] = tt_fma(rj, v - zn, y[gi][s]);
+                    z[gi][s] = zn;
+                }
+        }
+    };
+    // The plain (non-info) paired iteration.  It runs on the scaled dual yt = y / rho (the y registers
+    // hold yt between info iterations) and folds alpha into the KKT step, which takes the VALU work
+    // per element from 3 (x) / 7 (z, y) to 2 / 4 (the f32 matrix and vector pipes share the SIMD, so
+    // vector instructions cost MFMA time):
+    //   w~  = rho ((z - yt)_top - (z - yt)_bot)
+    //   xi  = (-g + S x') + B~' w~ ;  eta' = alpha dk xi ;  x' = eta' + (1 - alpha) x'
+    //   zt' = B~ eta' (= alpha z~_top, z~_bot = -z~_top)
+    //   t = (1 - alpha) z + zt' + yt ;  z = min(t, u) ;  yt = t - z
+    // (OSQP: z = min(alpha z~ + (1 - alpha) z + y / rho, u), y += rho (alpha z~ + (1 - alpha) z - z_new)).
+    // sx = -g + S x' of the NEXT iteration is issued right after x' so that its MFMAs run beside the
+    // z/y update.
+    auto piter_fast = [&](const T (&rS)[NTR][KNR], const T (&rBt)[NTR][KNR], const T (&rB)[NTR][KNR],
+                          T (&sx)[G][NS], const T (&adk)[G][KNR]) {
+        if constexpr (PAIRED) {
+            T wt[G][KNR];
+#pragma unroll
+            for (int gi = 0; gi < G; gi++)
+#pragma unroll
+                for (int s = 0; s < KN; s++)
+                    wt[gi][s] = rho[gi] * ((z[gi][s] - y[gi][s]) - (z[gi][s + KN] - y[gi][s + KN]));
+            T xi[G][NS];
+            reg_mv<T, G, NT, KN, KNR, false>(rBt, wt, rBt, wt, xi, sx);  // xi = (-g + S x') + B~' w~
+#pragma unroll
+            for (int gi = 0; gi < G; gi++)
+#pragma unroll
+                for (int s = 0; s < KN; s++) {
+                    xi[gi][s] = adk[gi][s] * xi[gi][s];           // eta' = alpha eta
+                    xs[gi][s] = tt_fma(oma, xs[gi][s], xi[gi][s]);  // x' = alpha eta + (1 - alpha) x'
+                }
+            T zt[G][NS];
+            reg_mv<T, G, NT, KN, NS, false>(rB, xi, rB, wt, zt, nullptr);  // alpha z~_top = B~ eta'
+            reg_mv<T, G, NT, KN, NS, false>(rS, xs, rS, wt, sx, gv);       // next: -g + S x'
+#pragma unroll
+            for (int gi = 0; gi < G; gi++)
+#pragma unroll
+                for (int s = 0; s < KM; s++) {
+                    const T v = s < KN ? tt_fma(oma, z[gi][s], zt[gi][s]) : tt_fma(oma, z[gi][s], -zt[gi][s - KN]);
+                    const T t = v + y[gi][s];
+                    const T zn = vmin(t, uh[gi][s]);
+                    y[gi][s] = t - zn;
+                    z[gi][s] = zn;
+                }
+        }
+    };
+    MPCQ_TSTAMP(2, (long long)__builtin_amdgcn_s_memtime());
     while (!all_done()) {
+        if constexpr (PAIRED) {
+            // plain iterations up to the next info iteration, with the operators held in VGPRs
+            // (loaded here, dead across the check code below)
+            int nxt = st.max_iter < stop ? st.max_iter : stop;
+            if (ct && next_check < nxt) nxt = next_check;
+            if (ai && next_adapt < nxt) nxt = next_adapt;
+            if (it + 1 < nxt) {
+                T rS[NTR][KNR], rBt[NTR][KNR], rB[NTR][KNR];
+                load_regs(rS, rBt, rB);
+                T sx[G][NS], adk[G][KNR];
+                reg_mv<T, G, NT, KN, NS, false>(rS, xs, rS, xs, sx, gv);
+#pragma unroll
+                for (int gi = 0; gi < G; gi++) {
+#pragma unroll
+                    for (int s = 0; s < KN; s++) adk[gi][s] = alpha * dk[gi][s];
+#pragma unroll
+                    for (int s = 0; s < KM; s++) y[gi][s] = y[gi][s] * rinv[gi];  // y -> yt = y / rho
+                }
+                do {
+                    it++;
+                    piter_fast(rS, rBt, rB, sx, adk);
+                } while (it + 1 < nxt);
+#pragma unroll
+                for (int gi = 0; gi < G; gi++)
+#pragma unroll
+                    for (int s = 0; s < KM; s++) y[gi][s] = y[gi][s] * rho[gi];  // yt -> y
+            }
+        }
         it++;
         const bool at_check = it == next_check;
         const bool at_adapt = it == next_adapt;
@@ -448,9 +711,14 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
 
         // ---- one ADMM iteration; the check iterations also keep delta_x', delta_y (OSQP's
         // delta_x / delta_y, for the infeasibility certificates)
-        T dx[G][NS], dy[G][MS];
         auto iterate = [&](auto with_delta) {
             constexpr bool DELTA = decltype(with_delta)::value;
+            if constexpr (PAIRED) {
+                T rS[NTR][KNR], rBt[NTR][KNR], rB[NTR][KNR];
+                load_regs(rS, rBt, rB);
+                piter(with_delta, rS, rBt, rB);
+                return;
+            }
             // xi = -g + sigma W'W x' + B' w,   w_j = rho_j z_j - y_j   (w reuses the zt registers)
             T wz[G][MS];
 #pragma unroll
@@ -532,12 +800,20 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
             tile_mv_g<T, G, NT, KN, KNP>(img + L.PW, xs, px, lane, nullptr);
             tile_mv_g<T, G, NT, KM, KMP>(img + L.AhT, y, aty, lane, nullptr);
             const T *Dinv = fresh_ptr((const T *)s_Dinv);
+            const double *qsrc = a.mpc ? a.q_out : a.q;  // this QP's q (written by the prologue in MPC mode)
 #pragma unroll
             for (int gi = 0; gi < G; gi++) {
+                T qh[NS];
+                const int b = opaque(b_[gi]);
+#pragma unroll
+                for (int s = 0; s < KN; s++) {
+                    const int v = 4 * s + g;
+                    qh[s] = v < n ? (T)((qsrc[(size_t)b * n + v] * (double)s_D[v]) * c64) : T(0);
+                }
                 dr_r[gi] = dr_s[gi] = qn_r[gi] = qn_s[gi] = atyn_r[gi] = atyn_s[gi] = pxn_r[gi] = pxn_s[gi] = T(0);
 #pragma unroll
                 for (int s = 0; s < KN; s++) {
-                    const T qhs = qh[gi][s];
+                    const T qhs = qh[s];
                     const T r = (qhs + px[gi][s]) + aty[gi][s];
                     const T di = Dinv[4 * s + g];
                     dr_r[gi] = nrm(dr_r[gi], r);
@@ -761,6 +1037,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
             for (int gi = 0; gi < G; gi++) done[gi] = term[gi];
         }
         if (it == stop && !all_done()) {
+            MPCQ_TSTAMP(3, (long long)__builtin_amdgcn_s_memtime());
             // phase boundary: save the running QPs and queue them for the next launch
 #pragma unroll
             for (int gi = 0; gi < G; gi++) {
@@ -790,6 +1067,9 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
             break;
         }
     }
+    MPCQ_TSTAMP(4, (long long)__builtin_amdgcn_s_memtime());
+    MPCQ_TSTAMP(5, (long long)it);
+    MPCQ_TSTAMP(7, (long long)__builtin_amdgcn_s_memrealtime());
 }
 
 // occ: 0 = default for the shape/type, else a requested variant (benchmark A/B hook):
@@ -799,6 +1079,21 @@ int tile_launch(const AdmmArgs<T> &a, int occ, hipStream_t s)
 {
     const dim3 block(256);
     auto grid = [&](int G) { return dim3((a.batch + 64 * G - 1) / (64 * G)); };
+    if constexpr (KM == 2 * KN) {
+        if (a.paired && a.all_ineq && a.lower_free) {  // the condensed-MPC shape: paired, VGPR-resident loop
+            if constexpr (sizeof(T) == 8) {
+                hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 1, 2, true>), grid(1), block, 0, s, a);
+            } else {
+                if (occ == 2)
+                    hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 2, 2, true>), grid(2), block, 0, s, a);
+                else if (occ == 4)
+                    hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 1, 4, true>), grid(1), block, 0, s, a);
+                else
+                    hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 1, 3, true>), grid(1), block, 0, s, a);
+            }
+            return hipGetLastError() == hipSuccess ? 0 : -2;
+        }
+    }
     if (a.all_ineq && a.lower_free) {
         if constexpr (sizeof(T) == 8) {
             if (occ == 1)

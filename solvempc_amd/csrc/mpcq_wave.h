@@ -10,9 +10,9 @@
 // rows a lane needs live in its VGPRs for the whole solve (row k of sigma W'W and column k of
 // B = A^ W for the x-side product, row j of B for the z-side product).  The two broadcasts of an
 // iteration (x' and w, then eta) go through LDS (one write per lane, 16-B broadcast reads).  Lane
-// reductions (residual norms, certificates) are DPP + permlane swaps.  The arithmetic, including
-// its order (sequential fused multiply-adds over i then j), is the tile kernel's, so a QP can move
-// from a tile launch to a wave launch at a phase boundary without changing its trajectory.
+// reductions (residual norms, certificates) are DPP + permlane swaps.  A QP can move from a tile
+// launch to a wave launch at a phase boundary: both run OSQP's iteration on the same state (x', z, y,
+// rho), with the products summed in different orders (last-bit differences, like any two OSQP builds).
 #pragma once
 #include "mpcq_tile.h"
 
@@ -51,21 +51,24 @@ template <typename T> __device__ __forceinline__ T wsum(T v)
 __device__ __forceinline__ int wor(int v) { return wave_any(v != 0) ? 1 : 0; }
 
 // acc + sum_i row[i] * bc[i] over the whole capacity: rows are zero beyond n / m and so are the
-// broadcast buffers, so the padding terms are exact no-ops (fixed trip count, no branches).
+// broadcast buffers, so the padding terms are exact no-ops (fixed trip count, no branches).  Four
+// interleaved partial sums (i mod 4) keep the dependent-FMA chain at CAP / 4: this product is the
+// latency of a lone QP's iteration (the tail of a shared-plant solve).
 template <typename T, int CAP>
 __device__ __forceinline__ T row_dot(const T (&row)[CAP], const T *bc, T acc)
 {
     constexpr int VEC = 16 / sizeof(T);
     typedef T vec __attribute__((ext_vector_type(VEC)));
     bc += opaque(0);  // a divergent address: keep the broadcast values in VGPRs (not SGPR copies)
+    T p[4] = {acc, T(0), T(0), T(0)};
 #pragma unroll
     for (int i0 = 0; i0 < CAP; i0 += VEC) {
         const vec v = *(const vec *)(bc + i0);
 #pragma unroll
         for (int e = 0; e < VEC; e++)
-            if (i0 + e < CAP) acc = tt_fma(row[i0 + e], v[e], acc);
+            if (i0 + e < CAP) p[(i0 + e) & 3] = tt_fma(row[i0 + e], v[e], p[(i0 + e) & 3]);
     }
-    return acc;
+    return (p[0] + p[1]) + (p[2] + p[3]);
 }
 
 // acc + sum_i M[i * stride] * bc[i] for i < CAP, M a zero-padded global operator column/row (cold
@@ -262,8 +265,7 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
         if (ln) bcx[lane] = xs;
         if (lm) bcw[lane] = w;
         __syncthreads();
-        T xi = row_dot(Srow, bcx, gk);
-        xi = row_dot(Btrow, bcw, xi);
+        T xi = row_dot(Srow, bcx, gk) + row_dot(Btrow, bcw, T(0));  // two independent chains
         const T eta = xi * dk;
         const T xn = ln ? tt_fma(alpha, eta, oma * xs) : T(0);
         const T dx = xn - xs;

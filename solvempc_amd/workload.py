@@ -117,12 +117,15 @@ def reference_plant(path=None) -> dict:
     }
 
 
-def flops_per_qp(n: int, m: int, nx: int, iters: np.ndarray, check: int = 25) -> np.ndarray:
+def flops_per_qp(n: int, m: int, nx: int, iters: np.ndarray, check: int = 25, paired: bool = False) -> np.ndarray:
     """Algorithmic FLOPs of one solve: iters*F_iter + checks*F_check + front end.
     F_iter = 4nm + 2n^2 + 9m + 6n; F_check = 4nm + 2n^2 + 6m + 4n; front end (q, u, W'q^)
-    = 2n(nx+1+n) + 2m(nx+1) + 2n^2.  No refactorisation FLOPs: rho updates are diagonal."""
+    = 2n(nx+1+n) + 2m(nx+1) + 2n^2.  No refactorisation FLOPs: rho updates are diagonal.
+    paired: the tile kernel's paired loop (rows n + j of A = -rows j) performs B'w and B eta over
+    m/2 rows, F_iter = 2nm + 2n^2 + 9m + 6n (the reduced count it actually performs; SURVEY §8d asks
+    for it when the A structure is exploited); its check iterations keep the dense F_check."""
     it = np.asarray(iters, dtype=np.float64)
-    f_iter = 4 * n * m + 2 * n * n + 9 * m + 6 * n
+    f_iter = (2 if paired else 4) * n * m + 2 * n * n + 9 * m + 6 * n
     f_check = 4 * n * m + 2 * n * n + 6 * m + 4 * n
     f_front = 2 * n * (nx + 1 + n) + 2 * m * (nx + 1) + 2 * n * n
     return it * f_iter + np.floor(it / check) * f_check + f_front

@@ -301,11 +301,13 @@ def test_dual_infeasible(kernel):
 
 
 def test_tile_and_wave_paths_agree(plant):
-    """A QP may move from a tile launch to a wave launch at a phase boundary: both kernels run the
-    same arithmetic in the same order, so whole solves agree (fp32 and fp64)."""
+    """A QP may move from a tile launch to a wave launch at a phase boundary: both kernels run OSQP's
+    iteration on the same state, with products summed in different orders (the tile kernel's paired
+    loop uses the +-row structure of A).  fp64: the same status and iteration count for every QP and
+    |dx| <= 1e-9; fp32: >= 99% of QPs on the same iteration schedule, within 1e-5 * max(1, |x|)."""
     N = 20
     ops, X, U, q, u = _problem(plant, N, 2048, seed=21)
-    for dtype, tol in (("f64", 1e-12), ("f32", 1e-5)):
+    for dtype in ("f64", "f32"):
         res = {}
         for k in ("tile", "wave"):
             os.environ["MPCQ_KERNEL"] = k
@@ -314,9 +316,16 @@ def test_tile_and_wave_paths_agree(plant):
                 res[k] = (s.solution(), *s.info())
             finally:
                 os.environ.pop("MPCQ_KERNEL", None)
-        assert np.array_equal(res["tile"][2], res["wave"][2])  # iterations
-        assert np.array_equal(res["tile"][1], res["wave"][1])  # status
-        assert np.abs(res["tile"][0] - res["wave"][0]).max() <= tol
+        (xt, stt, itt, _), (xw, stw, itw, _) = res["tile"], res["wave"]
+        assert np.all(stt == sm.SOLVED) and np.all(stw == sm.SOLVED)
+        if dtype == "f64":
+            assert np.array_equal(itt, itw)
+            assert np.abs(xt - xw).max() <= 1e-9
+        else:
+            same = itt == itw
+            assert same.mean() >= 0.99, f"{same.mean():.3%} on the same schedule"
+            rel = np.abs(xt[same] - xw[same]).max(axis=1) / np.maximum(1.0, np.abs(xw[same]).max(axis=1))
+            assert rel.max() < 1e-5
 
 
 def test_plant_simulation_matches_host(plant):
@@ -520,3 +529,17 @@ def test_stream_graph_recaptured_after_replant(plant):
                     Uk[b] += r.x()[0]
             np.testing.assert_allclose(Ud.cpu().numpy(), Uk, rtol=0, atol=1e-9, err_msg=f"phase {phase} step {k}")
             Xk = Xd.cpu().numpy().reshape(B, nx).copy()
+
+
+def test_paired_tile_path_selected(plant):
+    """The reference's constraint matrix Gbar = [K0 L; -K0 L] (ModelPredictiveControlAPI.cpp:332-347)
+    puts a shared-plant batch on the tile kernel's paired loop; a generic A does not."""
+    N = 20
+    ops, X, U, q, u = _problem(plant, N, 64)
+    s = _gpu_solve(ops, q, u, N, dtype="f32")
+    assert s.path() == ("tile", True)
+    A = ops["A"].copy()
+    A[N + 3, 0] *= 1.0000001  # no longer an exact negation of row 3
+    s2 = sm.BatchSolver(N, 2 * N, 64, dtype="f32")
+    s2.setup(ops["P"], np.zeros(N), A, np.full(2 * N, LMIN), ops["W0"])
+    assert s2.path() == ("tile", False)

@@ -1,10 +1,11 @@
-"""Latency/throughput probes of the tile kernel (dev tool, run on the GPU box).
+"""Latency/throughput probes of the shared-plant ADMM kernels (dev tool, run on the GPU box).
 
-Times fixed-iteration solves (eps = 0 => every QP runs exactly max_iter iterations) at several batch
-sizes and check intervals, so the per-iteration and per-check costs can be separated."""
+Fixed-iteration solves (eps = 0, adaptive rho off: every QP runs exactly `iters` iterations, one
+launch: MPCQ_PHASES=0) timed with HIP events on the launch stream, at several batch sizes, so that
+T(B, iters) = fixed(B) + iters * per_iter(B) separates launch/prologue cost from the loop."""
 import json
+import os
 import sys
-import time
 from pathlib import Path
 
 import numpy as np
@@ -15,36 +16,47 @@ from solvempc_amd import mpc, workload  # noqa: E402
 
 
 def main():
+    import torch
+
+    os.environ.setdefault("MPCQ_PHASES", "0")
     dtype = sys.argv[1] if len(sys.argv) > 1 else "f32"
+    batches = [int(b) for b in (sys.argv[2].split(",") if len(sys.argv) > 2 else (16, 16384, 49152, 65536))]
+    iters_list = [int(i) for i in (sys.argv[3].split(",") if len(sys.argv) > 3 else (25, 75, 125))]
     plant = workload.reference_plant()
     N = 20
     ops = mpc.condense({k: (plant[k][None] if k in ("Ad", "Bd", "Cd", "K") else [plant[k]])
                         for k in ("Ad", "Bd", "Cd", "K", "Q", "R", "RD")}, N)
     ops = {k: v[0] for k, v in ops.items()}
     l = np.full(2 * N, -np.finfo(np.float64).max)
-    out = []
-    for B in (16, 4096, 65536):
+    stream = torch.cuda.current_stream()
+    for B in batches:
         X, U = workload.mpc_states(1, 0, B)
         q = X @ ops["Fx"].T + U[:, None] * ops["Fu"]
         u = ops["W0"] + X @ ops["Sbar"].T + U[:, None] * ops["Ku"]
-        for ct, it in ((1, 100), (25, 100), (100, 100), (200, 200)):
-            st = sm.default_settings(eps_abs=0.0, eps_rel=1e-30, max_iter=it, check_termination=ct,
-                                     adaptive_rho=0)
+        res = []
+        for it in iters_list:
+            st = sm.default_settings(eps_abs=0.0, eps_rel=1e-30, max_iter=it, adaptive_rho=0)
             s = sm.BatchSolver(N, 2 * N, B, dtype=dtype, settings=st)
             s.setup(ops["P"], np.zeros(N), ops["A"], l, ops["W0"])
             s.update_lin_cost(q)
             s.update_upper_bound(u)
             ts = []
-            for rep in range(4):
+            for rep in range(5):
                 s.reset_state()
-                s.info()
-                t0 = time.perf_counter()
-                s.solve()
-                s.info()
-                ts.append(time.perf_counter() - t0)
-            rec = {"B": B, "ct": ct, "iters": it, "ms": 1e3 * min(ts[1:])}
-            out.append(rec)
-            print(json.dumps(rec), flush=True)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                s.solve(stream.cuda_stream)
+                e1.record(stream)
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1) * 1e3)
+            res.append((it, min(ts[1:])))
+            s.close()
+        its = np.array([r[0] for r in res], float)
+        us = np.array([r[1] for r in res])
+        slope, icpt = np.polyfit(its, us, 1) if len(its) > 1 else (us[0] / its[0], 0.0)
+        rec = {"B": B, "dtype": dtype, "us": {int(a): round(b, 2) for a, b in res}, "us_per_iter": round(slope, 3),
+               "fixed_us": round(icpt, 2), "kernel": os.environ.get("MPCQ_KERNEL", "default")}
+        print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":
