@@ -193,6 +193,25 @@ int mpcq_mpc_setup_plants_device(mpcq_ctx *ctx, int nx, int s_rows, const double
                                  const double *Bd, const double *Cd, const double *K,
                                  const double *Q, const double *R, const double *RD, void *stream);
 
+/* ---- MIMO condensed MPC (BASELINE config 4: quad-rotor hover linearisations, n_x 12, n_u 4, N 30) --
+ * The reference's condensing (ModelPredictiveControlAPI.cpp:158-369) with every SISO scalar a block
+ * (oracle/mpc_mimo.h): decision du in R^(N n_u), A = [L (x) K0; -(L (x) K0)], u = W0 + Sbar X + Ku U,
+ * l = -DBL_MAX.  The context must have n_plants == batch, n = N n_u (<= 128), m = 2n, dtype MPCQ_F64;
+ * n_u in {1, 2, 4}, n_x, n_y <= 12, N <= 32.
+ * Setup (replaces the ctor :3-65 + initSolver :64 per plant) from device-resident plant data,
+ * plant-major fp64: Ad nx*nx, Bd nx*nu, Cd ny*nx, Q ny*ny (symmetric), R nu*nu, RD nu*nu, K nu*nx,
+ * K0 nu*nu, w0 nu; S = K on block rows k < s_rows.  Condensing, Ruiz scaling and P^ on the device;
+ * the solver state is reset (x = z = y = 0, rho = settings.rho). */
+int mpcq_mimo_setup_plants_device(mpcq_ctx *ctx, int nx, int nu, int ny, int s_rows, const double *Ad,
+                                  const double *Bd, const double *Cd, const double *Q, const double *R,
+                                  const double *RD, const double *K, const double *K0, const double *w0,
+                                  void *stream);
+/* One controllerStep (:81-108) for every QP on device-resident X (batch*nx) and U (batch*nu):
+ * q = Fx X + Fu U + Fr (1_N (x) yref), u = W0 + Sbar X + Ku U, solve (warm-started after the first
+ * step), U += x[0:n_u] where SOLVED.  yref: device pointer to n_y values, or NULL for 0. */
+int mpcq_mimo_step_device(mpcq_ctx *ctx, const double *X_dev, double *U_dev, const double *yref_dev,
+                          void *stream);
+
 /* Last HIP error string of this thread (static storage). */
 const char *mpcq_last_error(void);
 

@@ -5,6 +5,8 @@ ctypes binding of the plain-C CPU checker in this directory:
 * ``mpc_condense.c`` restates the condensed-QP construction of LukeSchmitt96/solveMPC
   (src/ModelPredictiveControlAPI.cpp:111-375), pinned against the known-answer values of
   SURVEY.md Appendix B;
+* ``mpc_mimo.c`` generalises that construction to n_u inputs / n_y outputs (BASELINE config 4; no
+  reference counterpart — its SISO specialisation is ``mpc_condense.c``'s arithmetic);
 * ``osqp_dense.c`` restates OSQP v0.6's ADMM (the un-vendored solver behind
   ModelPredictiveControlAPI.cpp:51-64,96-105) in dense fp64.  PARITY UNPINNED at that
   boundary (no OSQP build, no reference fixtures); certified by KKT optimality checks.
@@ -59,6 +61,15 @@ class _Plant(C.Structure):
     ]
 
 
+class _MimoPlant(C.Structure):
+    _fields_ = [("nx", C.c_int), ("nu", C.c_int), ("ny", C.c_int), ("N", C.c_int), ("s_rows", C.c_int)] + \
+               [(k, C.POINTER(C.c_double)) for k in ("Ad", "Bd", "Cd", "Q", "R", "RD", "K", "K0", "w0")]
+
+
+class _MimoOps(C.Structure):
+    _fields_ = [(k, C.POINTER(C.c_double)) for k in ("P", "A", "Fx", "Fu", "Fr", "Sbar", "Ku", "W0", "Su")]
+
+
 class _Ops(C.Structure):
     _fields_ = [(k, C.POINTER(C.c_double)) for k in
                 ("P", "A", "Fx", "Fu", "Fr", "Sbar", "Ku", "W0", "Su", "Sx")]
@@ -71,7 +82,7 @@ def lib() -> C.CDLL:
         return _LIB
     so = _HERE / "liboracle.so"
     srcs = [_HERE / f for f in ("mpc_condense.c", "osqp_dense.c", "mpc_batch.c", "mpc_condense.h", "osqp_dense.h",
-                                "mpc_batch.h")]
+                                "mpc_batch.h", "mpc_mimo.c", "mpc_mimo.h")]
     if not so.exists() or any(s.stat().st_mtime > so.stat().st_mtime for s in srcs if s.exists()):
         subprocess.run(["make", "-C", str(_HERE), "-s"], check=True)
     L = C.CDLL(str(so))
@@ -104,6 +115,11 @@ def lib() -> C.CDLL:
     L.ora_plants_step.restype = C.c_int
     L.ora_plants_step.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, dp, dp, dp, dp, C.c_double, C.c_double,
                                   C.c_double, dp, dp, C.c_double, C.POINTER(Settings), dp, ip, ip, C.c_int]
+    L.ora_condense_mimo.restype = C.c_int
+    L.ora_condense_mimo.argtypes = [C.POINTER(_MimoPlant), C.POINTER(_MimoOps)]
+    L.ora_mimo_plants_step.restype = C.c_int
+    L.ora_mimo_plants_step.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, dp, dp, dp, dp, dp, dp,
+                                       dp, dp, dp, dp, dp, dp, C.POINTER(Settings), dp, dp, ip, ip, C.c_int]
     _LIB = L
     return L
 
@@ -172,6 +188,64 @@ def upper_bound(ops: dict, X, U) -> np.ndarray:
     X = np.asarray(X, dtype=np.float64)
     U = np.asarray(U, dtype=np.float64)
     return ops["W0"] + X @ ops["Sbar"].T + U[..., None] * ops["Ku"]
+
+
+MIMO_KEYS = ("Ad", "Bd", "Cd", "Q", "R", "RD", "K", "K0", "w0")
+
+
+def mimo_dims(plant: dict) -> tuple[int, int, int]:
+    Bd = np.asarray(plant["Bd"])
+    return Bd.shape[0], Bd.shape[1], np.asarray(plant["Cd"]).shape[0]
+
+
+def condense_mimo(plant: dict, N: int, s_rows: int | None = None) -> dict:
+    """MIMO condensed operators (mpc_mimo.h): plant dict with Ad (nx,nx), Bd (nx,nu), Cd (ny,nx),
+    Q (ny,ny), R, RD (nu,nu), K (nu,nx), K0 (nu,nu), w0 (nu)."""
+    nx, nu, ny = mimo_dims(plant)
+    keep = {k: _c64(plant[k]) for k in MIMO_KEYS}
+    pl = _MimoPlant(nx, nu, ny, N, N if s_rows is None else s_rows, *[_dp(keep[k]) for k in MIMO_KEYS])
+    n, m = N * nu, 2 * N * nu
+    shapes = {"P": (n, n), "A": (m, n), "Fx": (n, nx), "Fu": (n, nu), "Fr": (n, N * ny), "Sbar": (m, nx),
+              "Ku": (m, nu), "W0": (m,), "Su": (N * ny, n)}
+    out = {k: np.zeros(sh, dtype=np.float64) for k, sh in shapes.items()}
+    ops = _MimoOps(*[_dp(out[k]) for k in ("P", "A", "Fx", "Fu", "Fr", "Sbar", "Ku", "W0", "Su")])
+    if lib().ora_condense_mimo(C.byref(pl), C.byref(ops)) != 0:
+        raise ValueError("condense_mimo failed")
+    return out
+
+
+def mimo_gradient(ops: dict, X, U, yref=None) -> np.ndarray:
+    """q = Fx X + Fu U + Fr (1_N (x) yref).  Batched in X, U."""
+    X, U = np.asarray(X, dtype=np.float64), np.asarray(U, dtype=np.float64)
+    ny_tot = ops["Fr"].shape[1]
+    ref = np.zeros(ny_tot) if yref is None else np.tile(np.asarray(yref, dtype=np.float64), ny_tot // len(yref))
+    return X @ ops["Fx"].T + U @ ops["Fu"].T + ops["Fr"] @ ref
+
+
+def mimo_upper_bound(ops: dict, X, U) -> np.ndarray:
+    X, U = np.asarray(X, dtype=np.float64), np.asarray(U, dtype=np.float64)
+    return ops["W0"] + X @ ops["Sbar"].T + U @ ops["Ku"].T
+
+
+def mimo_plants_step(shared: dict, Ad, Bd, X, U, N: int, yref=None, settings: Settings | None = None,
+                     nthreads: int = 0, s_rows: int | None = None):
+    """Per-plant MIMO batch (config 4): condense + setup + one controllerStep per plant.
+    Returns (U_new (k, nu), x (k, n), status, iters)."""
+    Ad, Bd, X, U = _c64(Ad), _c64(Bd), _c64(X), _c64(U)
+    k, nx, nu = Bd.shape
+    ny = np.asarray(shared["Cd"]).shape[0]
+    sh = {key: _c64(shared[key]) for key in ("Cd", "Q", "R", "RD", "K", "K0", "w0")}
+    yr = _c64(np.zeros(ny) if yref is None else yref)
+    s = settings or default_settings()
+    n = N * nu
+    U_out = np.zeros((k, nu))
+    x_out = np.zeros((k, n))
+    st = np.zeros(k, dtype=np.int32)
+    it = np.zeros(k, dtype=np.int32)
+    lib().ora_mimo_plants_step(k, nx, nu, ny, N, N if s_rows is None else s_rows, _dp(Ad), _dp(Bd), _dp(sh["Cd"]),
+                               _dp(sh["Q"]), _dp(sh["R"]), _dp(sh["RD"]), _dp(sh["K"]), _dp(sh["K0"]), _dp(sh["w0"]),
+                               _dp(X), _dp(U), _dp(yr), C.byref(s), _dp(U_out), _dp(x_out), _ip(st), _ip(it), nthreads)
+    return U_out, x_out, st, it
 
 
 # ----------------------------------------------------------------------------- OSQP restatement

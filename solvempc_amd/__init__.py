@@ -208,6 +208,23 @@ class BatchSolver:
                                                        C.c_void_p(stream or 0)), "mpcq_mpc_setup_plants_device")
         self.nx = int(nx)
 
+    # -- MIMO condensed MPC (BASELINE config 4; oracle/mpc_mimo.h formulation)
+    def mimo_setup_plants_device(self, nx: int, nu: int, ny: int, s_rows: int, Ad_ptr: int, Bd_ptr: int, Cd_ptr: int,
+                                 Q_ptr: int, R_ptr: int, RD_ptr: int, K_ptr: int, K0_ptr: int, w0_ptr: int,
+                                 stream: int | None = None) -> None:
+        """Condense and set up every plant on the device from device-resident, plant-major fp64 data
+        (Ad nx*nx, Bd nx*nu, Cd ny*nx, Q ny*ny, R, RD nu*nu, K nu*nx, K0 nu*nu, w0 nu)."""
+        ptrs = [C.c_void_p(p) for p in (Ad_ptr, Bd_ptr, Cd_ptr, Q_ptr, R_ptr, RD_ptr, K_ptr, K0_ptr, w0_ptr)]
+        _capi.check(lib().mpcq_mimo_setup_plants_device(self._ctx, int(nx), int(nu), int(ny), int(s_rows), *ptrs,
+                                                        C.c_void_p(stream or 0)), "mpcq_mimo_setup_plants_device")
+        self.nx, self.nu = int(nx), int(nu)
+
+    def mimo_step_device(self, X_ptr: int, U_ptr: int, yref_ptr: int = 0, stream: int | None = None) -> None:
+        """One controllerStep for every QP on device-resident X (batch, nx), U (batch, nu); asynchronous."""
+        _capi.check(lib().mpcq_mimo_step_device(self._ctx, C.c_void_p(X_ptr), C.c_void_p(U_ptr),
+                                                C.c_void_p(yref_ptr or 0), C.c_void_p(stream or 0)),
+                    "mpcq_mimo_step_device")
+
     def mpc_step_device(self, X_ptr: int, U_ptr: int, xref: float = 0.0, stream: int | None = None) -> None:
         """Same on device-resident fp64 buffers (e.g. torch tensors' data_ptr()); asynchronous."""
         _capi.check(lib().mpcq_mpc_step_device(self._ctx, C.c_void_p(X_ptr), C.c_void_p(U_ptr),

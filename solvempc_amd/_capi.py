@@ -19,6 +19,7 @@ EXPORTS = (
     "mpcq_get_scaling", "mpcq_device_view_get", "mpcq_mpc_set_operators", "mpcq_mpc_step_device",
     "mpcq_mpc_step", "mpcq_mpc_set_plant", "mpcq_mpc_simulate_device", "mpcq_mpc_run_device",
     "mpcq_condense", "mpcq_mpc_setup_plants_device", "mpcq_last_error", "mpcq_get_path",
+    "mpcq_mimo_setup_plants_device", "mpcq_mimo_step_device",
 )
 
 
@@ -84,6 +85,8 @@ def lib() -> C.CDLL:
         "mpcq_get_dual": (C.c_int, [vp, dp]),
         "mpcq_get_info": (C.c_int, [vp, ip, ip, dp]),
         "mpcq_get_scaling": (C.c_int, [vp, dp, dp, dp]),
+        "mpcq_mimo_setup_plants_device": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.c_int] + [vp] * 9 + [vp]),
+        "mpcq_mimo_step_device": (C.c_int, [vp, vp, vp, vp, vp]),
         "mpcq_get_path": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "mpcq_device_view_get": (C.c_int, [vp, C.POINTER(DeviceView)]),
         "mpcq_mpc_set_operators": (C.c_int, [vp, C.c_int, dp, dp, dp, dp, dp, dp]),

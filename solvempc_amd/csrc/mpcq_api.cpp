@@ -81,6 +81,10 @@ struct mpcq_ctx {
     unsigned long long gen = 1;
     struct { double *X, *U; double xref, noise; unsigned long long seed; long long first_qp; hipStream_t s;
              unsigned long long gen; } gkey{};
+    // MIMO condensed MPC (mpcq_mimo.hip): per-plant operator block, dims
+    double *d_mimo = nullptr;
+    int mimo_N = 0, mimo_nx = 0, mimo_nu = 0, mimo_ny = 0, mimo_srows = 0;
+    bool mimo_ready = false, mimo_only = false;
     // host copies of plant-0 scaling
     std::vector<double> hD, hE;
     double hc = 1.0;
@@ -274,7 +278,12 @@ int mpcq_create(const mpcq_dims *d, const mpcq_settings *s, mpcq_ctx **out)
         nc = 16 * ((KN + 3) / 4);
         mc = 16 * ((KM + 3) / 4);
     } else if (mpcq_internal_caps(d->n, std::max(d->m, 1), &nc, &mc) != 0) {
-        return fail(MPCQ_ERR_ARG, "n/m exceed the compiled kernel capacities (n <= 32, m <= 64)");
+        // larger per-plant QPs: only the MIMO condensed-MPC path (mpcq_mimo_*) serves them
+        if (!(d->n_plants == d->batch && d->n <= 128 && d->m == 2 * d->n && d->dtype == MPCQ_F64))
+            return fail(MPCQ_ERR_ARG, "n/m exceed the compiled kernel capacities (n <= 32, m <= 64; the MIMO "
+                                      "MPC path takes per-plant n <= 128, m = 2n, fp64)");
+        nc = d->n;
+        mc = d->m;
     }
 
     int ndev = 0;
@@ -293,6 +302,7 @@ int mpcq_create(const mpcq_dims *d, const mpcq_settings *s, mpcq_ctx **out)
     c->nc = nc;
     c->mc = mc;
     c->tile = tile;
+    c->mimo_only = !tile && (d->n > 32 || d->m > 64);
     c->KN = KN;
     c->KM = KM;
     const mpcq::OpsLayout L = mpcq::OpsLayout::make(nc, mc);
@@ -304,14 +314,15 @@ int mpcq_create(const mpcq_dims *d, const mpcq_settings *s, mpcq_ctx **out)
         if (!ok) return;
         if (hipMalloc(p, std::max<size_t>(bytes, 8)) != hipSuccess) ok = false;
     };
-    A((void **)&c->d_P, 8 * P * n * n);
-    A((void **)&c->d_q0, 8 * P * n);
-    A((void **)&c->d_A, 8 * P * m * n);
-    A((void **)&c->d_l0, 8 * P * m);
-    A((void **)&c->d_u0, 8 * P * m);
-    A((void **)&c->d_ops, 8 * P * L.total);
-    if (d->dtype == MPCQ_F32) A((void **)&c->d_ops32, 4 * P * L.total);
-    A((void **)&c->d_ctype, 4 * P * mc);
+    const size_t Pg = c->mimo_only ? 1 : P;  // mimo-only: the generic setup arrays are unused
+    A((void **)&c->d_P, 8 * Pg * n * n);
+    A((void **)&c->d_q0, 8 * Pg * n);
+    A((void **)&c->d_A, 8 * Pg * m * n);
+    A((void **)&c->d_l0, 8 * Pg * m);
+    A((void **)&c->d_u0, 8 * Pg * m);
+    A((void **)&c->d_ops, 8 * Pg * L.total);
+    if (d->dtype == MPCQ_F32) A((void **)&c->d_ops32, 4 * Pg * L.total);
+    A((void **)&c->d_ctype, 4 * Pg * mc);
     A((void **)&c->d_setup_status, 4 * P);
     A((void **)&c->d_flags, 4);
     A((void **)&c->d_q, 8 * B * n);
@@ -332,7 +343,7 @@ int mpcq_create(const mpcq_dims *d, const mpcq_settings *s, mpcq_ctx **out)
         A((void **)&c->d_list, 4 * 2 * B);
         A((void **)&c->d_counts, 4 * kMaxPhases);
         A((void **)&c->d_itstate, 4 * B);
-    } else {
+    } else if (!c->mimo_only) {
         A(&c->d_snx, es * B * nc);
         A(&c->d_sny, es * B * mc);
     }
@@ -354,7 +365,7 @@ int mpcq_destroy(mpcq_ctx *c)
                     c->d_setup_status, c->d_q, c->d_u, c->d_l, c->d_x, c->d_y, c->d_rho, c->d_status, c->d_iter,
                     c->d_xs, c->d_zs, c->d_ys, c->d_rhos, c->d_snx, c->d_sny, c->d_Fx, c->d_Fu, c->d_Fr,
                     c->d_Sbar, c->d_Ku, c->d_W0, c->d_X, c->d_U, c->d_img, c->d_list, c->d_counts,
-                    c->d_itstate, c->d_Ad, c->d_Bd, c->d_step, c->d_flags, c->d_stamps};
+                    c->d_itstate, c->d_Ad, c->d_Bd, c->d_step, c->d_flags, c->d_stamps, c->d_mimo};
     if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
     if (c->graph) (void)hipGraphDestroy(c->graph);
     for (void *p : ptrs)
@@ -452,6 +463,7 @@ int mpcq_setup(mpcq_ctx *c, const double *P, const double *q0, const double *A, 
 {
     int rc = check_ctx(c, false);
     if (rc) return rc;
+    if (c->mimo_only) return fail(MPCQ_ERR_ARG, "n > 32 per-plant contexts are served by mpcq_mimo_* only");
     const size_t Pn = c->dims.n_plants, n = c->dims.n, m = c->dims.m;
     if (!P || !q0 || (m && (!A || !l0 || !u0))) return fail(MPCQ_ERR_ARG, "null setup array");
     for (size_t i = 0; i < Pn * m; i++)
@@ -693,6 +705,7 @@ int mpcq_solve(mpcq_ctx *c, void *stream)
 {
     int rc = check_ctx(c, true);
     if (rc) return rc;
+    if (c->mimo_only) return fail(MPCQ_ERR_ARG, "n > 32 per-plant contexts are served by mpcq_mimo_* only");
     return launch_solve(c, (hipStream_t)stream, false, nullptr, nullptr, 0.0);
 }
 
@@ -1013,6 +1026,98 @@ int mpcq_mpc_setup_plants_device(mpcq_ctx *c, int nx, int s_rows, const double *
     c->gen++;
     c->mpc_ready = true;
     c->setup_done = true;
+    return MPCQ_OK;
+}
+
+
+int mpcq_mimo_setup_plants_device(mpcq_ctx *c, int nx, int nu, int ny, int s_rows, const double *Ad, const double *Bd,
+                                  const double *Cd, const double *Q, const double *R, const double *RD, const double *K,
+                                  const double *K0, const double *w0, void *stream)
+{
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    const int n = c->dims.n, m = c->dims.m;
+    if (nu != 1 && nu != 2 && nu != 4) return fail(MPCQ_ERR_ARG, "mimo: n_u must be 1, 2 or 4");
+    if (nx <= 0 || nx > 12 || ny <= 0 || ny > 12 || s_rows < 0) return fail(MPCQ_ERR_ARG, "mimo: 1 <= n_x, n_y <= 12");
+    if (n % nu || n / nu > 32 || n > 128 || m != 2 * n) return fail(MPCQ_ERR_ARG, "mimo: n = N n_u <= 128 (N <= 32), m = 2n");
+    if (c->dims.n_plants != c->dims.batch || c->dims.dtype != MPCQ_F64)
+        return fail(MPCQ_ERR_ARG, "mimo: one plant per QP (n_plants == batch), dtype MPCQ_F64");
+    if (!Ad || !Bd || !Cd || !Q || !R || !RD || !K || !K0 || !w0) return fail(MPCQ_ERR_ARG, "mimo: null plant array");
+    const int N = n / nu;
+    const mpcq::MimoLayout L = mpcq::MimoLayout::make(N, nx, nu, ny);
+    if (c->d_mimo && (c->mimo_N != N || c->mimo_nx != nx || c->mimo_nu != nu || c->mimo_ny != ny)) {
+        (void)hipFree(c->d_mimo);
+        c->d_mimo = nullptr;
+    }
+    if (!c->d_mimo && hipMalloc((void **)&c->d_mimo, 8 * (size_t)L.total * c->dims.n_plants) != hipSuccess)
+        return fail(MPCQ_ERR_HIP, "hipMalloc failed (mimo operator blocks)");
+    c->mimo_N = N; c->mimo_nx = nx; c->mimo_nu = nu; c->mimo_ny = ny; c->mimo_srows = s_rows;
+    c->mimo_ready = false;
+    c->gen++;
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipMemsetAsync(c->d_flags, 0, 4, s));
+    mpcq::MimoSetupArgs a{};
+    a.n_plants = c->dims.n_plants;
+    a.N = N; a.nx = nx; a.nu = nu; a.ny = ny; a.s_rows = s_rows;
+    a.scaling = c->set.scaling;
+    a.sigma = c->set.sigma;
+    a.Ad = Ad; a.Bd = Bd; a.Cd = Cd; a.Q = Q; a.R = R; a.RD = RD; a.K = K; a.K0 = K0; a.w0 = w0;
+    a.ops = c->d_mimo;
+    a.flags = c->d_flags;
+    const int lr = mpcq_internal_mimo_setup_launch(&a, s);
+    if (lr == -1) return fail(MPCQ_ERR_ARG, "mimo: shape beyond the setup kernel's LDS capacity");
+    if (lr) return fail(MPCQ_ERR_HIP, std::string("mimo setup launch failed: ") + hipGetErrorString(hipGetLastError()));
+    int flags = 0;
+    HIPCHK(hipMemcpyAsync(&flags, c->d_flags, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (flags & 2) return fail(MPCQ_ERR_SETUP, "mimo: a constraint row is not an inequality (|w0| beyond OSQP_INFTY)");
+    c->last = s;
+    c->fresh = true;  // the first step starts from x = z = y = 0, rho = settings.rho (initSolver, :64)
+    c->mimo_ready = true;
+    c->setup_done = true;
+    return MPCQ_OK;
+}
+
+int mpcq_mimo_step_device(mpcq_ctx *c, const double *X, double *U, const double *yref, void *stream)
+{
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    if (!c->mimo_ready) return fail(MPCQ_ERR_ORDER, "mpcq_mimo_setup_plants_device has not succeeded");
+    if (!X || !U) return fail(MPCQ_ERR_ARG, "null X/U");
+    mpcq::MimoArgs a{};
+    a.batch = c->dims.batch;
+    a.N = c->mimo_N; a.nx = c->mimo_nx; a.nu = c->mimo_nu; a.ny = c->mimo_ny; a.s_rows = c->mimo_srows;
+    a.ops_stride = (size_t)mpcq::MimoLayout::make(a.N, a.nx, a.nu, a.ny).total;
+    a.ops = c->d_mimo;
+    a.st = to_solver(c->set);
+    const int ct = c->set.check_termination;
+    a.adaptive_interval = c->set.adaptive_rho_interval ? c->set.adaptive_rho_interval : (ct ? 4 * ct : 100);
+    a.X = X; a.U = U; a.yref = yref;
+    a.q_out = c->d_q; a.u_out = c->d_u;
+    a.xs = (double *)c->d_xs; a.zs = (double *)c->d_zs; a.ys = (double *)c->d_ys; a.rhos = (double *)c->d_rhos;
+    a.warm = c->set.warm_start;
+    a.fresh = c->fresh;
+    a.x = c->d_x; a.y = c->d_y; a.status = c->d_status; a.iter = c->d_iter; a.rho_out = c->d_rho;
+    const char *stp = std::getenv("MPCQ_MIMO_STAMPS");  // debug hook: per-QP stage stamps
+    if (stp && *stp) {
+        if (!c->d_stamps && hipMalloc((void **)&c->d_stamps, 8 * 8 * (size_t)a.batch) != hipSuccess)
+            return fail(MPCQ_ERR_HIP, "hipMalloc failed (stamps)");
+        a.stamps = c->d_stamps;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    const int lr = mpcq_internal_mimo_solve_launch(&a, s);
+    if (lr) return fail(lr == -1 ? MPCQ_ERR_ARG : MPCQ_ERR_HIP, "mimo solve launch failed");
+    if (stp && *stp) {
+        std::vector<long long> h(8 * (size_t)a.batch);
+        HIPCHK(hipMemcpyAsync(h.data(), c->d_stamps, 8 * h.size(), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (FILE *f = std::fopen(stp, "wb")) {
+            std::fwrite(h.data(), 8, h.size(), f);
+            std::fclose(f);
+        }
+    }
+    c->last = s;
+    c->fresh = false;
     return MPCQ_OK;
 }
 

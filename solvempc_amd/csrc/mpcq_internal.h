@@ -198,6 +198,65 @@ struct CondenseArgs {
 };
 }  // namespace mpcq
 
+namespace mpcq {
+// ---- MIMO condensed MPC (BASELINE config 4; mpcq_mimo.hip) -------------------------------------
+// Per-plant operator block (fp64, offsets in doubles) written by mimo_setup_kernel: the scaled Hessian
+// P^ = c D P D (row-major n x n), the Ruiz scaling (D: n; E: n, the same for row j and row n + j of
+// A = [L (x) K0; -(L (x) K0)]), c and 1/c, the unscaled front-end operators Fx (n x nx), Fu (n x nu),
+// Frs = Fr (1_N (x) I_ny) (n x ny), the bound data K (nu x nx), K0 (nu x nu), w0 (nu), and
+// SW (N blocks of nu x nu): suffix sums over k >= j of K0' diag(2 E_k^2) K0, so that the constraint
+// Gram matrix A^'A^ has block (j1, j2) = D SW[max(j1, j2)] D.
+struct MimoLayout {
+    int N, nx, nu, ny, n;
+    int Ph, D, E, cs, Fx, Fu, Frs, K, K0, w0, SW, total;  // < 2^31 for n <= 128
+    __host__ __device__ static MimoLayout make(int N, int nx, int nu, int ny)
+    {
+        MimoLayout L{};
+        L.N = N; L.nx = nx; L.nu = nu; L.ny = ny; L.n = N * nu;
+        const int n = L.n;
+        int o = 0;
+        L.Ph = o; o += n * n;
+        L.D = o; o += n;
+        L.E = o; o += n;
+        L.cs = o; o += 2;
+        L.Fx = o; o += n * nx;
+        L.Fu = o; o += n * nu;
+        L.Frs = o; o += n * ny;
+        L.K = o; o += nu * nx;
+        L.K0 = o; o += nu * nu;
+        L.w0 = o; o += nu;
+        L.SW = o; o += N * nu * nu;
+        L.total = (o + 1) & ~1;  // 16-B aligned blocks
+        return L;
+    }
+};
+
+struct MimoSetupArgs {
+    int n_plants, N, nx, nu, ny, s_rows, scaling;
+    double sigma;
+    const double *Ad, *Bd, *Cd, *Q, *R, *RD, *K, *K0, *w0;  // [plant] nx*nx, nx*nu, ny*nx, ny*ny, nu*nu x2, nu*nx, nu*nu, nu
+    double *ops;                                            // [plant] MimoLayout::total
+    int *flags;                                             // OR: 1 setup failed, 2 a row is not an inequality
+};
+
+struct MimoArgs {
+    int batch, N, nx, nu, ny, s_rows;
+    size_t ops_stride;
+    const double *ops;          // [plant] MimoLayout
+    SolverSettings st;
+    int adaptive_interval;
+    const double *X, *yref;     // batch*nx (device), ny (device)
+    double *U;                  // batch*nu (device): U += x[0:nu] when solved (:105)
+    double *q_out, *u_out;      // batch*n, batch*2n: this step's q, u (unscaled)
+    double *xs, *zs, *ys, *rhos;// scaled state (warm start): batch*n, batch*2n, batch*2n, batch
+    int warm, fresh;
+    double *x, *y;              // unscaled solution: batch*n, batch*2n
+    int *status, *iter;
+    double *rho_out;
+    long long *stamps;          // debug (MPCQ_MIMO_STAMPS) or null
+};
+}  // namespace mpcq
+
 // Launchers (extern "C" so the host library links them without templates).
 extern "C" {
 int mpcq_internal_setup_launch(const mpcq::SetupArgs *args, hipStream_t stream);
@@ -229,6 +288,10 @@ int mpcq_internal_simulate(int batch, int nx, int shared, const double *Ad, cons
                            long long step_v, double noise_std, hipStream_t s);
 int mpcq_internal_tick(long long *step, hipStream_t s);
 int mpcq_internal_set_step(long long *step, long long v, hipStream_t s);
+// MIMO condensed MPC (mpcq_mimo.hip): per-plant condensing + Ruiz + P^, then the per-QP solve
+// (one 512-thread workgroup per QP: KKT inverse by Gauss-Jordan in VGPRs, structured A).
+int mpcq_internal_mimo_setup_launch(const mpcq::MimoSetupArgs *a, hipStream_t s);
+int mpcq_internal_mimo_solve_launch(const mpcq::MimoArgs *a, hipStream_t s);
 // Build the TileLayout images (type T = f32 if is_f32) of plant 0 from its fp64 operator block.
 int mpcq_internal_tile_images(const double *ops, int nc, int mc, int KN, int KM, int is_f32, void *img,
                               hipStream_t s);

@@ -137,3 +137,78 @@ def flops_plant_setup(n: int, m: int, N: int | None = None) -> float:
     system; the eigen-basis setup does more work than this and is not credited for it)."""
     N = n if N is None else N
     return (4 * N ** 3 + 10 * N ** 2 + 128 * N) + 30 * (n * n + n * m) + (2 * n * n * m + n ** 3 / 3 + n * n)
+
+
+# ----------------------------------------------------------------------------- config 4: quad-rotor
+QUAD = {  # hover linearisation of a small quad-rotor (BASELINE config 4: n_x 12, n_u 4, N 30, dt 0.02)
+    "mass": 0.5, "inertia": (2.3e-3, 2.3e-3, 4.0e-3), "g": 9.81, "dt": 0.02, "spread": 0.10,
+    # outputs y = x (Cd = I); weights: position 10, attitude 1, velocity 1, body rates 0.1
+    "q_diag": (10.0, 10.0, 10.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 0.1, 0.1, 0.1),
+    "r_diag": (0.1, 10.0, 10.0, 10.0), "rd_diag": (1.0, 100.0, 100.0, 100.0),
+    # input box |u_k| <= w0 around hover: thrust deviation [N], roll/pitch/yaw torque [N m]
+    "w0": (2.0, 0.05, 0.05, 0.02),
+}
+# State X ~ N(0, diag(s^2)): position 0.3 m, attitude 0.1 rad, velocity 0.3 m/s, rates 0.3 rad/s;
+# the applied input U ~ U(-w0/2, w0/2).
+QUAD_X_STD = np.array([0.3, 0.3, 0.3, 0.1, 0.1, 0.1, 0.3, 0.3, 0.3, 0.3, 0.3, 0.3])
+
+
+def quadrotor_continuous(mass: float, Ixx: float, Iyy: float, Izz: float, g: float = 9.81):
+    """Hover linearisation, x = [p (3), (phi, theta, psi), v (3), body rates (3)], u = [thrust deviation,
+    tau_phi, tau_theta, tau_psi]: p' = v, angles' = rates, vx' = g theta, vy' = -g phi, vz' = T / m,
+    rates' = tau / I."""
+    A = np.zeros((12, 12))
+    A[0, 6] = A[1, 7] = A[2, 8] = 1.0
+    A[3, 9] = A[4, 10] = A[5, 11] = 1.0
+    A[6, 4] = g
+    A[7, 3] = -g
+    B = np.zeros((12, 4))
+    B[8, 0] = 1.0 / mass
+    B[9, 1], B[10, 2], B[11, 3] = 1.0 / Ixx, 1.0 / Iyy, 1.0 / Izz
+    return A, B
+
+
+def zoh(A, B, dt: float):
+    """Exact zero-order-hold discretisation: exp([[A, B], [0, 0]] dt) by its Taylor series (the
+    augmented hover matrix is nilpotent, so the series terminates: exact up to rounding)."""
+    nx, nu = B.shape
+    M = np.zeros((nx + nu, nx + nu))
+    M[:nx, :nx], M[:nx, nx:] = A * dt, B * dt
+    E, T = np.eye(nx + nu), np.eye(nx + nu)
+    for k in range(1, 24):
+        T = T @ M / k
+        if not T.any():
+            break
+        E = E + T
+    return E[:nx, :nx], E[:nx, nx:]
+
+
+def quadrotor_plants(seed: int, start: int, count: int):
+    """Config 4 plants for global indices start .. start+count-1: mass and the three inertias scaled
+    by U(1 - spread, 1 + spread) each (counter-based draws 0..3), ZOH at dt.  Returns Ad (count, 12, 12),
+    Bd (count, 12, 4)."""
+    q = QUAD
+    u = uniforms(seed, start, count, 4)
+    f = 1.0 + q["spread"] * (2.0 * u - 1.0)
+    Ad = np.empty((count, 12, 12))
+    Bd = np.empty((count, 12, 4))
+    for i in range(count):
+        A, B = quadrotor_continuous(q["mass"] * f[i, 0], q["inertia"][0] * f[i, 1], q["inertia"][1] * f[i, 2],
+                                    q["inertia"][2] * f[i, 3], q["g"])
+        Ad[i], Bd[i] = zoh(A, B, q["dt"])
+    return Ad, Bd
+
+
+def quadrotor_shared() -> dict:
+    """The weights and constraint data shared by every config-4 plant (mpc_mimo.h names): Cd = I,
+    Q, R, RD diagonal, K = 0 (no state term in the bounds), K0 = I (box on the applied input), w0."""
+    q = QUAD
+    return {"Cd": np.eye(12), "Q": np.diag(q["q_diag"]), "R": np.diag(q["r_diag"]), "RD": np.diag(q["rd_diag"]),
+            "K": np.zeros((4, 12)), "K0": np.eye(4), "w0": np.array(q["w0"], dtype=np.float64)}
+
+
+def quadrotor_states(seed: int, start: int, count: int):
+    """Config 4 states X ~ N(0, diag(QUAD_X_STD^2)) and applied inputs U ~ U(-w0/2, w0/2)."""
+    X = normals(seed, start, count, 12) * QUAD_X_STD
+    U = (uniforms(seed ^ 0x5A5A, start, count, 4) - 0.5) * np.array(QUAD["w0"])
+    return X, U

@@ -148,3 +148,34 @@ def test_plants_step_matches_per_plant_solver(plant):
         assert st[b] == s and it[b] == r.info().iter
         # (numpy's q/u products round differently from the C loops in the last bits)
         assert abs(Uo[b] - (U[b] + r.x()[0] if s == 1 else U[b])) < 1e-12
+
+
+def test_mimo_condensing_siso_specialisation_is_bit_identical(plant):
+    """oracle/mpc_mimo.c at n_u = n_y = 1, K0 = K(0), w0 = 255 reproduces the reference-pinned SISO
+    condensing (mpc_condense.c, ModelPredictiveControlAPI.cpp:180-369) bit for bit."""
+    for N in (15, 20):
+        ref = oracle.condense(plant, N)
+        mp = {"Ad": plant["Ad"], "Bd": plant["Bd"][:, None], "Cd": plant["Cd"][None, :], "Q": [[plant["Q"]]],
+              "R": [[plant["R"]]], "RD": [[plant["RD"]]], "K": plant["K"][None, :], "K0": [[plant["K"][0]]],
+              "w0": [255.0]}
+        mo = oracle.condense_mimo(mp, N, s_rows=10)
+        for k in ("P", "A", "Fx", "Fr", "Sbar", "W0", "Su"):
+            assert np.array_equal(mo[k].reshape(ref[k].shape), ref[k]), (N, k)
+        assert np.array_equal(mo["Fu"][:, 0], ref["Fu"]) and np.array_equal(mo["Ku"][:, 0], ref["Ku"])
+
+
+def test_quadrotor_plants_and_oracle_solve():
+    """Config 4 plants: exact ZOH of the hover model (the augmented matrix is nilpotent), mass/inertia
+    spread within +-10%, and the oracle solves every sampled QP."""
+    from solvempc_amd import workload
+
+    Ad, Bd = workload.quadrotor_plants(3, 0, 8)
+    A, B = workload.quadrotor_continuous(0.5, 2.3e-3, 2.3e-3, 4e-3)
+    Ad0, Bd0 = workload.zoh(A, B, 0.02)
+    assert np.allclose(Ad0, Ad[0])  # Ad does not depend on mass / inertia
+    f = workload.QUAD["mass"] / (1.0 / Bd[:, 8, 0] * 0.02)  # Bd[8, 0] = dt / m
+    assert np.all(np.abs(f - 1.0) <= 0.1 + 1e-12)
+    X, U = workload.quadrotor_states(3, 0, 8)
+    Un, x, st, it = oracle.mimo_plants_step(workload.quadrotor_shared(), Ad, Bd, X, U, 30, nthreads=4)
+    assert np.all(st == oracle.SOLVED)
+    assert np.all(np.abs(Un) <= np.array(workload.QUAD["w0"]) + 1e-3)  # the applied input stays in the box
