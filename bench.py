@@ -39,10 +39,12 @@ def parse():
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=0)
-    p.add_argument("--workload", choices=("cfg2", "stream", "perplant"), default="cfg2",
+    p.add_argument("--workload", choices=("cfg2", "stream", "perplant", "quadrotor"), default="cfg2",
                    help="cfg2: BASELINE config 2 (the headline); stream: config 5 (4,096 plants x --ctrl-steps "
                         "warm-started control steps with a simulated plant, hipGraph-replayed); perplant: config 3 "
-                        "(randomised plants, per-GPU shard of 1M: condense + setup + one controllerStep each)")
+                        "(randomised plants, per-GPU shard of 1M: condense + setup + one controllerStep each); "
+                        "quadrotor: config 4 (262,144 quad-rotor hover linearisations, n_x 12, n_u 4, N 30: MIMO "
+                        "condense + setup + one controllerStep each, fp64)")
     p.add_argument("--ctrl-steps", type=int, default=1000, help="control steps per bench step (stream)")
     p.add_argument("--noise", type=float, default=1e-2, help="plant noise std (stream; SURVEY §8d: var 1e-4)")
     a = p.parse_args()
@@ -52,6 +54,14 @@ def parse():
         a.batch = 131072  # 1,048,576 / 8 GPUs
         if a.seed == 1:
             a.seed = 2  # SURVEY §8d config 3 seed
+    if a.workload == "quadrotor":
+        if a.batch == 65536:
+            a.batch = 262144  # BASELINE config 4
+        if a.horizon == 20:
+            a.horizon = 30
+        if a.seed == 1:
+            a.seed = 3  # SURVEY §8d config 4 seed
+        a.dtype = "f64"
     return a
 
 
@@ -95,6 +105,143 @@ def cpu_baseline_plants(plant, Ad, Bd, N, X, U, budget_s, threads):
                       f"setup + solve, fp64, OpenMP {nthr} threads, {dt:.2f} s"}
 
 
+def cpu_baseline_quadrotor(shared, Ad, Bd, X, U, N, budget_s, threads):
+    """The oracle's MIMO per-plant path (condense + OSQP-0.6 setup + one controllerStep, fp64 C,
+    OpenMP) on a bounded sample of the config-4 plants."""
+    import oracle
+
+    nthr = threads or min(16, os.cpu_count() or 1)
+    n = 64
+    while True:
+        t0 = time.perf_counter()
+        oracle.mimo_plants_step(shared, Ad[:n], Bd[:n], X[:n], U[:n], N, nthreads=nthr)
+        dt = time.perf_counter() - t0
+        if dt > budget_s / 4 or n >= len(X):
+            break
+        n = min(len(X), int(n * max(2.0, budget_s / 4 / max(dt, 1e-3))))
+    return {"value": n / dt, "unit": "QP/s", "cores": nthr, "kind": "port",
+            "sample": f"{n} plants of the same batch (first {n}): oracle/mpc_mimo.c condense + osqp_dense.c "
+                      f"setup + solve, fp64, OpenMP {nthr} threads, {dt:.2f} s"}
+
+
+def main_quadrotor(a, rank, world, local, dist, dev):
+    """BASELINE config 4: every QP its own quad-rotor plant (hover linearisation with +-10% mass and
+    inertia, ZOH dt 0.02); one step = device condensing + setup of every plant + one controllerStep
+    each (mpcq_mimo_setup_plants_device + mpcq_mimo_step_device), fp64."""
+    import torch
+
+    import solvempc_amd as sm
+    from solvempc_amd import dist as mdist
+    from solvempc_amd import workload
+
+    N, B = a.horizon, a.batch
+    nu = 4
+    start, count = mdist.weak_block(B, rank)
+    Ad, Bd = workload.quadrotor_plants(a.seed, start, count)
+    sh = workload.quadrotor_shared()
+    X, U = workload.quadrotor_states(a.seed, start, count)
+    nx, ny = Ad.shape[1], np.asarray(sh["Cd"]).shape[0]
+    tdev = lambda v: torch.as_tensor(np.ascontiguousarray(v, dtype=np.float64)).to(dev)  # noqa: E731
+    plant_d = [tdev(Ad), tdev(Bd)] + [
+        torch.as_tensor(np.asarray(sh[k], dtype=np.float64)).to(dev).expand((B,) + np.asarray(sh[k]).shape).contiguous()
+        for k in ("Cd", "Q", "R", "RD", "K", "K0", "w0")]
+    solver = sm.BatchSolver(N * nu, 2 * N * nu, B, B, "f64", local)
+    X_d, U0_d = tdev(X), tdev(U)
+    U_d = U0_d.clone()
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+    gathered = [torch.empty_like(U_d) for _ in range(world)] if rank == 0 else None
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    ev_mid = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
+
+    def step(i=None):
+        U_d.copy_(U0_d)  # the reference's first control step of each plant (setup resets the solver)
+        if i is not None:
+            ev[i][0].record(stream)
+        solver.mimo_setup_plants_device(nx, nu, ny, N, *[t.data_ptr() for t in plant_d], stream=sptr)
+        if i is not None:
+            ev_mid[i].record(stream)
+        solver.mimo_step_device(X_d.data_ptr(), U_d.data_ptr(), 0, sptr)
+        if i is not None:
+            ev[i][1].record(stream)
+        mdist.gather_moves(dist, U_d, world, rank, gathered)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([wall], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    setup_ms = float(np.mean([s.elapsed_time(m_) for (s, _), m_ in zip(ev, ev_mid)]))
+    solve_ms = float(np.mean([m_.elapsed_time(e) for (_, e), m_ in zip(ev, ev_mid)]))
+    status, iters, rho = solver.info()
+    n = N * nu
+    # factorisations: the initial inverse plus (at least) one per QP whose rho moved
+    fact = 1 + (rho != solver.settings.rho)
+    setup_flops = B * workload.flops_mimo_setup(N, nx, nu, ny, solver.settings.scaling)
+    solve_flops = float(workload.flops_mimo_solve(n, nu, iters, fact).sum())
+    dense = float(workload.flops_mimo_dense(N, nx, nu, ny, iters).sum())
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    tf = lambda f, ms: f / (ms * 1e-3) / 1e12  # noqa: E731
+    peak = PEAK_TFLOPS["f64"]
+    rec = {
+        "metric": "QP solves/sec (quad-rotor n_x=12, n_u=4, N=30 batch)",
+        "value": B * world * a.steps / wall,
+        "unit": "QP/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": wall / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (hover linearisations, mass/inertia +-10% counter-based per plant; X ~ N(0, diag), U ~ U(-w0/2, w0/2))",
+        "config": {"workload": f"cfg4: {B} quad-rotor plants per GPU (n_x {nx}, n_u {nu}, n_y {ny}), N={N} "
+                               f"(n={n}, m={2 * n}): on-device MIMO condensing + setup + one controllerStep each",
+                   "batch_per_gpu": B, "horizon": N, "parallelism": f"dp{world}"},
+        # dominant stage: the per-QP solve (Gauss-Jordan KKT inverse + ADMM iterations, fp64 VALU)
+        "roofline": {"bound": "valu", "achieved": tf(solve_flops, solve_ms), "peak": peak, "unit": "TFLOP/s",
+                     "frac": tf(solve_flops, solve_ms) / peak, "traffic": None,
+                     "kernel": "mimo_solve_kernel (fp64 vector peak)", "kernel_ms": solve_ms,
+                     "flops_per_step": solve_flops,
+                     "flops_note": "algorithmic for the structured solve: 2n^3 per KKT inverse (1 + one per QP whose "
+                                   "rho adapted), iters x (2n^2 + structured A products + 30n) "
+                                   "(workload.flops_mimo_solve)"},
+        "stages": {"setup_ms": setup_ms, "solve_ms": solve_ms, "step_ms": kern_ms,
+                   "setup_roofline": {"bound": "valu", "achieved": tf(setup_flops, setup_ms), "peak": peak,
+                                      "unit": "TFLOP/s", "frac": tf(setup_flops, setup_ms) / peak,
+                                      "kernel": "mimo_setup_kernel", "flops_per_step": setup_flops,
+                                      "note": "timed span includes the host read-back of the setup status word"}},
+        "dense_equivalent": {"flops_per_step": dense, "achieved": tf(dense, kern_ms), "frac": tf(dense, kern_ms) / peak,
+                             "note": "SURVEY §8d count: dense condensing + Ruiz + one KKT LDL + iters x F_iter(n, m)"},
+        "iters": {"mean": float(iters.mean()), "max": int(iters.max()),
+                  "solved_frac": float(np.mean(status == sm.SOLVED)), "rho_adapted_frac": float(np.mean(fact > 1))},
+    }
+    if a.cpu_seconds > 0:
+        rec["cpu_baseline"] = cpu_baseline_quadrotor(sh, Ad, Bd, X, U, N, a.cpu_seconds, a.cpu_threads)
+    print(json.dumps(rec))
+    if dist:
+        dist.destroy_process_group()
+
+
 def traffic_per_solve(dtype, batch, N):
     """HBM bytes of one solve from the committed PMC pass (tools/pmc.sh -> profiles/), or None."""
     f = ROOT / "profiles" / f"pmc_traffic_{dtype}.json"
@@ -124,6 +271,8 @@ def main():
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if a.workload == "quadrotor":
+        return main_quadrotor(a, rank, world, local, dist, dev)
 
     import solvempc_amd as sm
     from solvempc_amd import workload

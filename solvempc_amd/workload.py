@@ -185,17 +185,22 @@ def zoh(A, B, dt: float):
 
 def quadrotor_plants(seed: int, start: int, count: int):
     """Config 4 plants for global indices start .. start+count-1: mass and the three inertias scaled
-    by U(1 - spread, 1 + spread) each (counter-based draws 0..3), ZOH at dt.  Returns Ad (count, 12, 12),
+    by U(1 - spread, 1 + spread) each (counter-based draws 0..3), ZOH at dt.  A does not depend on
+    mass or inertia, so Ad and Phi = int_0^dt exp(A s) ds are those of the nominal model (the
+    augmented series of zoh() with B = I) and Bd = Phi B(plant).  Returns Ad (count, 12, 12),
     Bd (count, 12, 4)."""
     q = QUAD
     u = uniforms(seed, start, count, 4)
     f = 1.0 + q["spread"] * (2.0 * u - 1.0)
-    Ad = np.empty((count, 12, 12))
-    Bd = np.empty((count, 12, 4))
-    for i in range(count):
-        A, B = quadrotor_continuous(q["mass"] * f[i, 0], q["inertia"][0] * f[i, 1], q["inertia"][1] * f[i, 2],
-                                    q["inertia"][2] * f[i, 3], q["g"])
-        Ad[i], Bd[i] = zoh(A, B, q["dt"])
+    A, _ = quadrotor_continuous(q["mass"], *q["inertia"], q["g"])
+    Ad0, Phi = zoh(A, np.eye(12), q["dt"])
+    Bc = np.zeros((count, 12, 4))
+    Bc[:, 8, 0] = 1.0 / (q["mass"] * f[:, 0])
+    Bc[:, 9, 1] = 1.0 / (q["inertia"][0] * f[:, 1])
+    Bc[:, 10, 2] = 1.0 / (q["inertia"][1] * f[:, 2])
+    Bc[:, 11, 3] = 1.0 / (q["inertia"][2] * f[:, 3])
+    Ad = np.broadcast_to(Ad0, (count, 12, 12)).copy()
+    Bd = np.einsum("ij,bjk->bik", Phi, Bc)
     return Ad, Bd
 
 
@@ -212,3 +217,41 @@ def quadrotor_states(seed: int, start: int, count: int):
     X = normals(seed, start, count, 12) * QUAD_X_STD
     U = (uniforms(seed ^ 0x5A5A, start, count, 4) - 0.5) * np.array(QUAD["w0"])
     return X, U
+
+
+def flops_mimo_setup(N: int, nx: int, nu: int, ny: int, scaling: int = 10) -> float:
+    """FLOPs mimo_setup_kernel performs per plant (structured condensing, mpcq_mimo.hip): the CS / Sx
+    recurrences, Fx, Q CS, the prefix-sum H, Fu, Frs, P assembly, and `scaling` Ruiz passes over P
+    (column norms twice, rescale once)."""
+    n = N * nu
+    rec = N * 2 * (ny * nu * nx + 2 * ny * nx * nx + nx * nu * nx + ny * nx * ny)
+    fx = sum(d + 1 for d in range(N)) * 2 * nu * nx * ny
+    qcs = N * 2 * ny * nu * ny
+    h = sum(N - d for d in range(N)) * 2 * nu * nu * ny
+    fu = sum(N - j for j in range(N)) * 2 * nu * nu * ny
+    frs = sum(N - j for j in range(N)) * nu * ny
+    ruiz = scaling * 3 * n * n
+    return float(rec + fx + qcs + h + fu + frs + 4 * n * n + ruiz)
+
+
+def flops_mimo_solve(n: int, nu: int, iters, factorisations, check: int = 25) -> np.ndarray:
+    """FLOPs mimo_solve_kernel performs per QP: 2 n^3 per Gauss-Jordan inverse of the reduced KKT
+    matrix (initial + one per adaptive-rho change), and per iteration the GEMV with M^-1 (2 n^2), the
+    structured A^ / A^' products (block scans and K0 products, 2 x (2 n nu + n log2(64/nu)) each, plus
+    A^'A^ x~ for the carried P^ x) and ~30 n of element-wise work; per check two more products and
+    the norms (~20 n)."""
+    it = np.asarray(iters, dtype=np.float64)
+    sc = 2 * n * nu + n * np.log2(64 / nu)
+    f_iter = 2 * n * n + 2 * sc + 30 * n
+    f_check = 2 * sc + 20 * n
+    return np.asarray(factorisations, dtype=np.float64) * 2 * n ** 3 + it * f_iter + np.floor(it / check) * f_check
+
+
+def flops_mimo_dense(N: int, nx: int, nu: int, ny: int, iters, check: int = 25) -> np.ndarray:
+    """Dense-equivalent count: dense condensing 2 (N nu)^2 (N ny) + Ruiz 10 x 3 (n^2 + nm)
+    + one KKT LDL 2 n^2 m + n^3 / 3 + n^2, and iters x F_iter + checks x F_check with
+    F_iter = 4nm + 2n^2 + 9m + 6n, F_check = 4nm + 2n^2 + 6m + 4n."""
+    n, m = N * nu, 2 * N * nu
+    it = np.asarray(iters, dtype=np.float64)
+    setup = 2 * n * n * (N * ny) + 30 * (n * n + n * m) + 2 * n * n * m + n ** 3 / 3 + n * n
+    return setup + it * (4 * n * m + 2 * n * n + 9 * m + 6 * n) + np.floor(it / check) * (4 * n * m + 2 * n * n + 6 * m + 4 * n)
