@@ -207,15 +207,16 @@ namespace mpcq {
 // SW (N blocks of nu x nu): suffix sums over k >= j of K0' diag(2 E_k^2) K0, so that the constraint
 // Gram matrix A^'A^ has block (j1, j2) = D SW[max(j1, j2)] D.
 struct MimoLayout {
-    int N, nx, nu, ny, n;
+    int N, nx, nu, ny, n, ldp;
     int Ph, D, E, cs, Fx, Fu, Frs, K, K0, w0, SW, total;  // < 2^31 for n <= 128
     __host__ __device__ static MimoLayout make(int N, int nx, int nu, int ny)
     {
         MimoLayout L{};
         L.N = N; L.nx = nx; L.nu = nu; L.ny = ny; L.n = N * nu;
         const int n = L.n;
+        L.ldp = (n + 15) & ~15;  // P^ rows padded (zeros) to 16 columns: aligned, in-bounds 16-column loads
         int o = 0;
-        L.Ph = o; o += n * n;
+        L.Ph = o; o += n * L.ldp;
         L.D = o; o += n;
         L.E = o; o += n;
         L.cs = o; o += 2;

@@ -15,12 +15,12 @@
 //    row / column norms are prefix / suffix maxima over the horizon).  Writes P^ = c D P D and the
 //    operator block of MimoLayout.
 //
-//  * mimo_solve_kernel — one 512-thread workgroup per QP.  The reduced KKT matrix
+//  * mimo_solve_kernel — one 256-thread workgroup per QP, two per CU.  The reduced KKT matrix
 //    M(rho) = P^ + sigma I + rho A^'A^ (A^'A^ from the suffix sums SW of the setup) lives in VGPRs as
-//    4 x 8 blocks (thread (rb, cb): rows 4 rb.., columns 8 cb..) and is inverted in place by
+//    4 x 16 blocks (thread (rg, cg): rows 4 rg.., columns 16 cg..) and is inverted in place by
 //    Gauss-Jordan (SPD: no pivoting; one LDS row/column broadcast and one barrier per step).  An ADMM
-//    iteration is then one GEMV with M^-1 (all 8 waves) plus O(n) vector work on wave 0, where A^ x
-//    and A^' w are block prefix / suffix scans (lane shuffles) and K0 products.  OSQP's adaptive rho
+//    iteration is then one GEMV with M^-1 (all 4 waves) plus O(n) vector work on wave 0 (lane k =
+//    horizon block k), where A^ x and A^' w are lane prefix / suffix scans (DPP) and K0 products.  OSQP's adaptive rho
 //    (adapt_rho at multiples of the interval) re-inverts M(rho_new) in place from P^ (global); the
 //    dual residual's P^ x is carried through the KKT identity P^ x~ = rhs - sigma x~ - rho A^'A^ x~
 //    (exact algebra; no P^ product per check).  Checks, certificates and statuses are OSQP v0.6's
@@ -276,7 +276,10 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
     }
 
     // ---- outputs: P^, D, E, c, SW (suffix sums of K0' diag(2 E_k^2) K0), row-type check
-    for (int e = t; e < n * n; e += T) out[L.Ph + e] = P[(size_t)(e / n) * ldp + e % n];
+    for (int e = t; e < n * L.ldp; e += T) {
+        const int i = e / L.ldp, j = e % L.ldp;
+        out[L.Ph + e] = j < n ? P[(size_t)i * ldp + j] : 0.0;
+    }
     for (int j = t; j < n; j += T) {
         out[L.D + j] = Dv[j];
         out[L.E + j] = Ev[j];
@@ -300,58 +303,75 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
 }
 
 // ----------------------------------------------------------------------------------------------
-// solve: one 512-thread workgroup per QP
-constexpr int kMimoThreads = 512;
-constexpr int kMimoN = 128;  // n capacity (M^-1 padded to 128 x 128: thread (rb, cb) holds rows
-                             // 4 rb .. 4 rb + 3, columns 8 cb .. 8 cb + 7)
+// solve: one 320-thread workgroup per QP (waves 0-3: the matrix; wave 4: the vector work), two QPs
+// per CU (<= 168 VGPRs: three waves per SIMD).
+//
+// M(rho) = P^ + sigma I + rho A^'A^ lives in the matrix waves' VGPRs, padded to 128 x 128 with the
+// identity: thread (rg, cg) = (t >> 3, t & 7) holds rows 4 rg .. 4 rg + 3, columns 16 cg .. 16 cg + 15
+// (64 doubles).  Gauss-Jordan inverts it in place (SPD: no pivoting), one LDS row / column broadcast
+// and one barrier per step; the step loop is unrolled by 16 so the owners of row / column k address
+// their registers with compile-time indices.  An ADMM iteration is one GEMV with M^-1 (the 8-lane
+// partial sums of a row group reduced by DPP) and O(n) work on the vector wave, where lane k holds
+// horizon block k (its NU components): A^ x and A^' w are lane prefix / suffix scans (DPP row shifts
+// plus one cross-row readlane) and per-lane K0 products.  The two roles run separate loops with the
+// same barrier sequence, so the matrix registers are never live in the vector wave's code.
+constexpr int kMimoThreads = 320;
+constexpr int kMimoMat = 256;
+constexpr int kMimoN = 128;       // n capacity
+constexpr int kMimoBlk = 64 * 4;  // block-major vector slots: lane k, component c at 4 k + c
 
-// Vector layout on wave 0: element e = lane + 64 s (s = 0, 1) of an n-vector; block k = e / nu,
-// component c = e % nu (nu divides 64, so both registers agree on c = lane % nu).
-struct V2 {
-    double v[2];
+struct B4 {
+    double v[4];
 };
 
-__device__ inline double shfl_up_d(double v, int d) { return __shfl_up(v, d, 64); }
-__device__ inline double shfl_down_d(double v, int d) { return __shfl_down(v, d, 64); }
-__device__ inline double shfl_d(double v, int l) { return __shfl(v, l, 64); }
-
-// inclusive prefix over blocks: S[e] = sum_{k' <= k(e)} v[k' nu + c(e)]  (padding elements must be 0)
-__device__ inline V2 blk_prefix(V2 x, int nu, int lane)
+__device__ __forceinline__ B4 ldb(const double *arr, int lane)
 {
-    for (int s = 0; s < 2; s++)
-        for (int d = nu; d < 64; d <<= 1) {
-            const double o = shfl_up_d(x.v[s], d);
-            if (lane >= d) x.v[s] += o;
-        }
-    x.v[1] += shfl_d(x.v[0], 64 - nu + lane % nu);
-    return x;
+    const double2 *p = (const double2 *)(arr + 4 * lane);
+    const double2 u = p[0], w = p[1];
+    return {{u.x, u.y, w.x, w.y}};
 }
-// inclusive suffix over blocks: S[e] = sum_{k' >= k(e)} v[k' nu + c(e)]
-__device__ inline V2 blk_suffix(V2 x, int nu, int lane)
+__device__ __forceinline__ void stb(double *arr, int lane, const B4 &x)
 {
-    for (int s = 0; s < 2; s++)
-        for (int d = nu; d < 64; d <<= 1) {
-            const double o = shfl_down_d(x.v[s], d);
-            if (lane + d < 64) x.v[s] += o;
-        }
-    x.v[0] += shfl_d(x.v[1], lane % nu);
-    return x;
+    double2 *p = (double2 *)(arr + 4 * lane);
+    p[0] = make_double2(x.v[0], x.v[1]);
+    p[1] = make_double2(x.v[2], x.v[3]);
 }
-// out[e] = sum_r K[r][c] in[k nu + r]  (trans: K0' per block)  or  sum_c K[r][c] in[k nu + c]
-// (plain: K0 per block, r = c(e)); K row-major nu x nu in LDS
-__device__ inline V2 blk_k0(V2 x, const double *K, int nu, int lane, bool trans)
+// DPP move whose lanes without a source read 0 (row shifts)
+template <int CTRL> __device__ __forceinline__ double dpp0(double v)
 {
-    V2 o;
-    const int c = lane % nu, base = lane - c;
-    for (int s = 0; s < 2; s++) {
-        double acc = 0.0;
-        for (int r = 0; r < nu; r++) {
-            const double w = trans ? K[r * nu + c] : K[c * nu + r];
-            acc += w * shfl_d(x.v[s], base + r);
-        }
-        o.v[s] = acc;
-    }
-    return o;
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xF, 0xF, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ double readlane_d(double v, int l)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// inclusive prefix over lanes 0..31 (horizon blocks; N <= 32): row_shr 1, 2, 4, 8, then row 1 adds
+// lane 15's total
+__device__ __forceinline__ double lane_prefix(double v, int lane)
+{
+    v += dpp0<0x111>(v);
+    v += dpp0<0x112>(v);
+    v += dpp0<0x114>(v);
+    v += dpp0<0x118>(v);
+    const double s = readlane_d(v, 15);
+    return (lane >= 16) ? v + s : v;
+}
+// inclusive suffix over lanes 0..31 (lanes N..31 must hold 0): row_shl 1, 2, 4, 8, then row 0 adds
+// lane 16's total
+__device__ __forceinline__ double lane_suffix(double v, int lane)
+{
+    v += dpp0<0x101>(v);
+    v += dpp0<0x102>(v);
+    v += dpp0<0x104>(v);
+    v += dpp0<0x108>(v);
+    const double s = readlane_d(v, 16);
+    return (lane < 16) ? v + s : v;
 }
 
 #define MPCQ_MSTAMP(k, v)                                                                  \
@@ -359,51 +379,237 @@ __device__ inline V2 blk_k0(V2 x, const double *K, int nu, int lane, bool trans)
         if (a.stamps && t == 0) a.stamps[(size_t)blockIdx.x * 8 + (k)] = (long long)(v);  \
     } while (0)
 
-__global__ __launch_bounds__(kMimoThreads, 2) void mimo_solve_kernel(MimoArgs a)
+template <int NU>
+__global__ __launch_bounds__(kMimoThreads, 3) void mimo_solve_kernel(MimoArgs a)
 {
     const int b = blockIdx.x;
     if (b >= a.batch) return;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const int rb = t >> 4, cb = t & 15;
-    const int N = a.N, nx = a.nx, nu = a.nu, ny = a.ny, n = N * nu, m = 2 * n;
-    const MimoLayout L = MimoLayout::make(N, nx, nu, ny);
+    const int N = a.N, nx = a.nx, ny = a.ny, n = N * NU, m = 2 * n;
+    const MimoLayout L = MimoLayout::make(N, nx, NU, ny);
     const double *ops = a.ops + (size_t)b * a.ops_stride;
     const SolverSettings &st = a.st;
     MPCQ_MSTAMP(0, __builtin_amdgcn_s_memtime());
 
-    // LDS: the GEMV's input / output, the Gauss-Jordan broadcasts, and wave 0's vector state (its
-    // registers are only live inside one vector phase; M^-1 keeps the VGPRs across the loop)
-    __shared__ __attribute__((aligned(16))) double s_vec[kMimoN];  // rhs (GEMV input)
+    __shared__ __attribute__((aligned(16))) double s_vec[kMimoN];  // GEMV input (natural order)
     __shared__ __attribute__((aligned(16))) double s_out[kMimoN];  // GEMV output
+    __shared__ __attribute__((aligned(16))) double s_nat[kMimoN];  // warm start: x (natural), then P^ x
     __shared__ __attribute__((aligned(16))) double s_row[2][kMimoN], s_col[2][kMimoN];
-    __shared__ double s_D[kMimoN], s_E[kMimoN], s_K0[16], s_SW[32 * 16];
-    __shared__ double s_x[kMimoN], s_zt[kMimoN], s_zb[kMimoN], s_yt[kMimoN], s_yb[kMimoN], s_px[kMimoN];
-    __shared__ double s_qh[kMimoN], s_ut[kMimoN], s_ub[kMimoN];
+    __shared__ __attribute__((aligned(16))) double s_D[kMimoBlk], s_E[kMimoBlk], s_K0[16], s_SW[32 * 16];
+    __shared__ __attribute__((aligned(16))) double s_x[kMimoBlk], s_zt[kMimoBlk], s_zb[kMimoBlk], s_yt[kMimoBlk];
+    __shared__ __attribute__((aligned(16))) double s_yb[kMimoBlk], s_px[kMimoBlk], s_qh[kMimoBlk], s_ut[kMimoBlk];
+    __shared__ __attribute__((aligned(16))) double s_ub[kMimoBlk], s_rhs[kMimoBlk];
+    __shared__ __attribute__((aligned(16))) double s_dx[kMimoBlk], s_dpx[kMimoBlk], s_dyt[kMimoBlk], s_dyb[kMimoBlk];
     __shared__ int s_ctrl[2];
     __shared__ double s_rho;
-    for (int i = t; i < kMimoN; i += kMimoThreads) {
-        s_D[i] = i < n ? ops[L.D + i] : 1.0;
-        s_E[i] = i < n ? ops[L.E + i] : 1.0;
+    for (int i = t; i < kMimoBlk; i += kMimoThreads) {
+        const int k = i >> 2, c = i & 3;
+        const bool ok = k < N && c < NU;
+        s_D[i] = ok ? ops[L.D + k * NU + c] : 1.0;
+        s_E[i] = ok ? ops[L.E + k * NU + c] : 1.0;
     }
-    for (int i = t; i < nu * nu; i += kMimoThreads) s_K0[i] = ops[L.K0 + i];
-    for (int i = t; i < N * nu * nu; i += kMimoThreads) s_SW[i] = ops[L.SW + i];
+    for (int i = t; i < 16; i += kMimoThreads) {
+        const int r = i >> 2, c = i & 3;
+        s_K0[i] = (r < NU && c < NU) ? ops[L.K0 + r * NU + c] : 0.0;
+    }
+    for (int i = t; i < 32 * 16; i += kMimoThreads) {
+        const int k = i >> 4, ci = (i >> 2) & 3, cj = i & 3;
+        s_SW[i] = (k < N && ci < NU && cj < NU) ? ops[L.SW + (k * NU + ci) * NU + cj] : 0.0;
+    }
+    for (int i = t; i < kMimoN; i += kMimoThreads) s_vec[i] = 0.0;
+    __syncthreads();
 
     const double c64 = ops[L.cs], cinv = ops[L.cs + 1];
     const double sigma = st.sigma, alpha = st.alpha, oma = 1.0 - st.alpha;
-    auto ld2 = [&](const double *arr) {
-        V2 v;
-        v.v[0] = arr[lane];
-        v.v[1] = arr[lane + 64];
-        return v;
-    };
-    auto st2 = [&](double *arr, const V2 &v) {
-        arr[lane] = v.v[0];
-        arr[lane + 64] = v.v[1];
-    };
+    int fail = 0;
+
+    if (wv < 4) {
+        // ======== waves 0-3: M(rho) and M^-1 in VGPRs
+        const int rg = t >> 3, cg = t & 7;
+        double Mb[4][16];
+        // rows 4 rg + i, columns 16 cg + j (P^ rows are padded to L.ldp: aligned, in-bounds loads);
+        // the padding beyond n is the identity
+        auto load_P = [&]() {
+            const int seg = 16 * cg < L.ldp - 16 ? 16 * cg : L.ldp - 16;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int gi = 4 * rg + i;
+                const double2 *row = (const double2 *)(ops + L.Ph + (size_t)(gi < n ? gi : n - 1) * L.ldp + seg);
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const double2 v = row[j];
+                    const int gj = 16 * cg + 2 * j;
+                    Mb[i][2 * j] = (gi < n && gj < n) ? v.x : (gi == gj ? 1.0 : 0.0);
+                    Mb[i][2 * j + 1] = (gi < n && gj + 1 < n) ? v.y : (gi == gj + 1 ? 1.0 : 0.0);
+                }
+            }
+        };
+        // + sigma I + r D SW[max(bi, bj)] D on the n x n part (block of row gi: (4 rg + i) / NU)
+        auto add_kkt = [&](double r) {
+            double di[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int bi = (4 * rg) / NU + i / NU;
+                di[i] = s_D[4 * (bi < 63 ? bi : 63) + i % NU];
+            }
+#pragma unroll
+            for (int jc = 0; jc < 4; jc++) {
+#pragma unroll
+                for (int jj = 0; jj < 4; jj++) {
+                    const int j = 4 * jc + jj, gj = 16 * cg + j;
+                    const int bj = (16 * cg) / NU + j / NU, cj = j % NU;
+                    const double dj = s_D[4 * (bj < 63 ? bj : 63) + cj];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const int gi = 4 * rg + i, bi = (4 * rg) / NU + i / NU, ci = i % NU;
+                        const int bm = bi > bj ? bi : bj;
+                        const double g = (di[i] * dj) * s_SW[(bm < 31 ? bm : 31) * 16 + ci * 4 + cj];
+                        const double v = Mb[i][j] + (gi == gj ? sigma : 0.0) + r * g;
+                        if (gi < n && gj < n) Mb[i][j] = v;
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int jj = 0; jj < 4; jj++) asm volatile("" : "+v"(Mb[i][4 * jc + jj]));  // (as in invert)
+            }
+        };
+        // outv[4 rg + i] = row (4 rg + i) of M . in (the 8 lanes of a row group combine by DPP)
+        auto gemv = [&](const double *in, double *outv) {
+            double s0[4], s1[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) s0[i] = s1[i] = 0.0;
+            const double2 *v2 = (const double2 *)(in + 16 * cg);
+#pragma unroll
+            for (int h = 0; h < 4; h++) {  // 4-column chunks (register budget)
+                const double2 p0 = v2[2 * h], p1 = v2[2 * h + 1];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    s0[i] = __builtin_fma(Mb[i][4 * h], p0.x, s0[i]);
+                    s1[i] = __builtin_fma(Mb[i][4 * h + 1], p0.y, s1[i]);
+                    s0[i] = __builtin_fma(Mb[i][4 * h + 2], p1.x, s0[i]);
+                    s1[i] = __builtin_fma(Mb[i][4 * h + 3], p1.y, s1[i]);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; i++) asm volatile("" : "+v"(s0[i]), "+v"(s1[i]));  // one chunk live at a time
+            }
+            double part[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                part[i] = s0[i] + s1[i];
+                part[i] += dpp_t<0xB1>(part[i]);   // quad_perm [1,0,3,2]
+                part[i] += dpp_t<0x4E>(part[i]);   // quad_perm [2,3,0,1]
+                part[i] += dpp_t<0x141>(part[i]);  // row_half_mirror: the other quad of the 8
+            }
+            if (cg == 0) {
+                double2 *o2 = (double2 *)(outv + 4 * rg);
+                o2[0] = make_double2(part[0], part[1]);
+                o2[1] = make_double2(part[2], part[3]);
+            }
+        };
+        // Gauss-Jordan: a_ij -= (a_ik / a_kk) a_kj everywhere, then row k <- a_kj / a_kk, column k <-
+        // -a_ik / a_kk, a_kk <- 1 / a_kk.  k = 16 kb + kk with kk unrolled: the owner of column k is
+        // cg == kb (register column kk), of row k rg == k >> 2 (register row kk & 3).
+        auto invert = [&]() {
+            const int nkb = (n + 15) >> 4;
+            for (int kb = 0; kb < nkb; kb++) {
+#pragma unroll
+                for (int kk = 0; kk < 16; kk++) {
+                    const int k = 16 * kb + kk;
+                    if (k >= n) continue;  // (not break: the loop must fully unroll, or Mb leaves the VGPRs)
+                    const int p = k & 1;
+                    const bool rown = rg == (k >> 2), coln = cg == kb;
+                    if (rown) {
+                        double2 *r2 = (double2 *)&s_row[p][16 * cg];
+#pragma unroll
+                        for (int j = 0; j < 8; j++) r2[j] = make_double2(Mb[kk & 3][2 * j], Mb[kk & 3][2 * j + 1]);
+                    }
+                    if (coln) {
+                        double2 *c2 = (double2 *)&s_col[p][4 * rg];
+                        c2[0] = make_double2(Mb[0][kk], Mb[1][kk]);
+                        c2[1] = make_double2(Mb[2][kk], Mb[3][kk]);
+                    }
+                    __syncthreads();
+                    const double piv = s_row[p][k];
+                    if (!(piv > 0.0)) fail = 1;
+                    const double inv = 1.0 / piv;
+                    double nci[4];  // -a_ik / a_kk
+                    {
+                        const double2 *c2 = (const double2 *)&s_col[p][4 * rg];
+                        const double2 u0 = c2[0], u1 = c2[1];
+                        nci[0] = -u0.x * inv;
+                        nci[1] = -u0.y * inv;
+                        nci[2] = -u1.x * inv;
+                        nci[3] = -u1.y * inv;
+                    }
+                    const double2 *r2 = (const double2 *)&s_row[p][16 * cg];
+#pragma unroll
+                    for (int h = 0; h < 4; h++) {  // 4-column chunks (register budget)
+                        const double2 q0 = r2[2 * h], q1 = r2[2 * h + 1];
+                        const double rj[4] = {q0.x, q0.y, q1.x, q1.y};
+#pragma unroll
+                        for (int i = 0; i < 4; i++)
+#pragma unroll
+                            for (int j = 0; j < 4; j++) Mb[i][4 * h + j] = __builtin_fma(nci[i], rj[j], Mb[i][4 * h + j]);
+                        // pin the updates here: sunk below the fix-up branches they would keep every
+                        // chunk of the row live (register budget)
+#pragma unroll
+                        for (int i = 0; i < 4; i++)
+#pragma unroll
+                            for (int j = 0; j < 4; j++) asm volatile("" : "+v"(Mb[i][4 * h + j]));
+                    }
+                    asm volatile("" ::: "memory");  // the row owners re-read the row below
+                    if (rown) {  // row k <- a_kj / a_kk (re-read: the row owners are one wave's 8 lanes)
+#pragma unroll
+                        for (int h = 0; h < 8; h++) {
+                            const double2 q = r2[h];
+                            Mb[kk & 3][2 * h] = q.x * inv;
+                            Mb[kk & 3][2 * h + 1] = q.y * inv;
+                        }
+                    }
+                    if (coln) {
+#pragma unroll
+                        for (int i = 0; i < 4; i++) Mb[i][kk] = nci[i];
+                        if (rown) Mb[kk & 3][kk] = inv;
+                    }
+                }
+            }
+        };
+
+        load_P();  // overlaps the vector wave's front end
+        __syncthreads();  // front end + first rhs done
+        MPCQ_MSTAMP(1, __builtin_amdgcn_s_memtime());
+        bool loaded = true;
+        for (;;) {
+            const int ctrl = s_ctrl[0];
+            if (ctrl == 2) break;
+            if (ctrl == 1) {  // (re-)invert M(s_rho); the first factorisation also forms P^ x of a warm start
+                if (!loaded) load_P();
+                loaded = false;
+                if (s_ctrl[1]) {
+                    __syncthreads();  // everyone has read s_ctrl[1]
+                    gemv(s_nat, s_out);
+                    __syncthreads();
+                    for (int i = t; i < kMimoN; i += kMimoMat) s_nat[i] = s_out[i];
+                    if (t == 0) s_ctrl[1] = 0;
+                }
+                add_kkt(s_rho);
+                invert();  // its first barrier orders the writes above before the GEMV below
+                MPCQ_MSTAMP(2, __builtin_amdgcn_s_memtime());
+                if (fail) break;  // P^ + sigma I + rho A^'A^ not positive definite
+            }
+            gemv(s_vec, s_out);
+            __syncthreads();  // x~ ready
+            __syncthreads();  // the vector wave's phase done (next rhs, control word)
+        }
+        return;
+    }
+
+    // ======== wave 4 (lane k = horizon block k): the MPC front end and the ADMM vector work
     double rho = 0.0;
     int status = kUnsolved;
-    // ---- wave 0: per-QP data (the MPC front end), state
-    if (wv == 0) {
+    const bool load = a.warm && !a.fresh;
+    {
         double Xv[12], Uv[4], yr[12];
 #pragma unroll
         for (int i = 0; i < 12; i++) {
@@ -411,248 +617,180 @@ __global__ __launch_bounds__(kMimoThreads, 2) void mimo_solve_kernel(MimoArgs a)
             yr[i] = (i < ny && a.yref) ? a.yref[i < ny ? i : 0] : 0.0;
         }
 #pragma unroll
-        for (int i = 0; i < 4; i++) Uv[i] = i < nu ? a.U[(size_t)b * nu + (i < nu ? i : 0)] : 0.0;
+        for (int i = 0; i < NU; i++) Uv[i] = a.U[(size_t)b * NU + i];
         int tchg = 0;
-        const bool load = a.warm && !a.fresh;
-        for (int s = 0; s < 2; s++) {
-            const int e = lane + 64 * s;
-            double qh = 0.0, uth = 0.0, ubh = 0.0, x = 0.0, zt = 0.0, zb = 0.0, yt = 0.0, yb = 0.0;
-            if (e < n) {
-                const int k = e / nu, r = e % nu;
-                const double De = s_D[e], Ee = s_E[e];
+        B4 qh, uth, ubh, x, zt, zb, yt, yb;
+        const int k = lane;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            qh.v[c] = uth.v[c] = ubh.v[c] = x.v[c] = zt.v[c] = zb.v[c] = yt.v[c] = yb.v[c] = 0.0;
+            if (c < NU && k < N) {
+                const int e = k * NU + c;
+                const double De = s_D[4 * k + c], Ee = s_E[4 * k + c];
                 // setF (:372-375): q = Fx X + Fu U + Fr ref, ref = 1_N (x) yref (updateRef :378-380)
                 double s0 = 0.0, s1 = 0.0, s2 = 0.0;
                 for (int i = 0; i < nx; i++) s0 += ops[L.Fx + (size_t)e * nx + i] * Xv[i];
-                for (int i = 0; i < nu; i++) s1 += ops[L.Fu + (size_t)e * nu + i] * Uv[i];
+#pragma unroll
+                for (int i = 0; i < NU; i++) s1 += ops[L.Fu + (size_t)e * NU + i] * Uv[i];
                 for (int i = 0; i < ny; i++) s2 += ops[L.Frs + (size_t)e * ny + i] * yr[i];
                 const double q = s0 + s1 + s2;
                 if (a.q_out) a.q_out[(size_t)b * n + e] = q;
-                qh = (q * De) * c64;
+                qh.v[c] = (q * De) * c64;
                 // (:93-99): u = W0 + Sbar X + Ku U; Sbar block rows k < s_rows = [K; -K]; Ku = [-K0; K0]
                 double kx = 0.0, k0u = 0.0;
                 if (k < a.s_rows)
-                    for (int i = 0; i < nx; i++) kx += ops[L.K + r * nx + i] * Xv[i];
-                for (int i = 0; i < nu; i++) k0u += ops[L.K0 + r * nu + i] * Uv[i];
-                const double w0 = ops[L.w0 + r];
+                    for (int i = 0; i < nx; i++) kx += ops[L.K + c * nx + i] * Xv[i];
+#pragma unroll
+                for (int i = 0; i < NU; i++) k0u += ops[L.K0 + c * NU + i] * Uv[i];
+                const double w0 = ops[L.w0 + c];
                 const double utop = w0 + kx + -k0u, ubot = w0 + -kx + k0u;
                 if (a.u_out) {
                     a.u_out[(size_t)b * m + e] = utop;
                     a.u_out[(size_t)b * m + n + e] = ubot;
                 }
-                uth = utop * Ee;
-                ubh = ubot * Ee;
+                uth.v[c] = utop * Ee;
+                ubh.v[c] = ubot * Ee;
                 // l = -DBL_MAX (:42): every row stays an inequality while u^ is finite
-                if (!(uth < kInfty * kMinScaling) || !(ubh < kInfty * kMinScaling)) tchg = 1;
+                if (!(uth.v[c] < kInfty * kMinScaling) || !(ubh.v[c] < kInfty * kMinScaling)) tchg = 1;
                 if (load) {
-                    x = a.xs[(size_t)b * n + e];
-                    zt = a.zs[(size_t)b * m + e];
-                    zb = a.zs[(size_t)b * m + n + e];
-                    yt = a.ys[(size_t)b * m + e];
-                    yb = a.ys[(size_t)b * m + n + e];
+                    x.v[c] = a.xs[(size_t)b * n + e];
+                    zt.v[c] = a.zs[(size_t)b * m + e];
+                    zb.v[c] = a.zs[(size_t)b * m + n + e];
+                    yt.v[c] = a.ys[(size_t)b * m + e];
+                    yb.v[c] = a.ys[(size_t)b * m + n + e];
                 }
+                s_nat[e] = x.v[c];
             }
-            s_qh[e] = qh; s_ut[e] = uth; s_ub[e] = ubh;
-            s_x[e] = x; s_zt[e] = zt; s_zb[e] = zb; s_yt[e] = yt; s_yb[e] = yb; s_px[e] = 0.0;
-            s_vec[e] = x;  // x for P^ x of a warm start
         }
+        stb(s_qh, lane, qh); stb(s_ut, lane, uth); stb(s_ub, lane, ubh);
+        stb(s_x, lane, x); stb(s_zt, lane, zt); stb(s_zb, lane, zb); stb(s_yt, lane, yt); stb(s_yb, lane, yb);
+        stb(s_px, lane, B4{{0.0, 0.0, 0.0, 0.0}});
         if (wave_any(tchg != 0)) status = kTypeChanged;
         rho = a.fresh ? fmin(fmax(st.rho, kRhoMin), kRhoMax) : a.rhos[b];
-        if (lane == 0) {
-            s_rho = rho;
-            s_ctrl[0] = status;
-            s_ctrl[1] = load ? 1 : 0;
-        }
     }
-    __syncthreads();
-    MPCQ_MSTAMP(1, __builtin_amdgcn_s_memtime());
 
-    // ---- M = P^ + sigma I + rho A^'A^ in VGPRs (4 x 8 block per thread), inverted by Gauss-Jordan
-    double Mb[4][8];
-    int fail = 0;
-    auto gemv = [&](const double *in, double *outv) {  // outv[4 rb + i] = sum_j Mb row i . in  (all threads)
-        double part[4];
-        const double2 *v2 = (const double2 *)(in + 8 * cb);
-        double w[8];
+    auto lmask = [&](B4 v) {
+        if (lane >= N)
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const double2 p = v2[j];
-            w[2 * j] = p.x;
-            w[2 * j + 1] = p.y;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-            for (int j = 0; j < 8; j += 2) {
-                s0 = __builtin_fma(Mb[i][j], w[j], s0);
-                s1 = __builtin_fma(Mb[i][j + 1], w[j + 1], s1);
-            }
-            part[i] = s0 + s1;
-        }
-#pragma unroll
-        for (int d = 8; d >= 1; d >>= 1)
-#pragma unroll
-            for (int i = 0; i < 4; i++) part[i] += __shfl_xor(part[i], d, 64);
-        if (cb == 0)
-#pragma unroll
-            for (int i = 0; i < 4; i++) outv[4 * rb + i] = part[i];
-    };
-    // nu is a power of two (<= 4): block / component of an index by shifts
-    const int lognu = nu == 1 ? 0 : (nu == 2 ? 1 : 2);
-    auto load_P = [&]() {
-        // rows 4 rb + i (clamped to n - 1), columns 8 cb + j: padding columns read the bytes that follow
-        // the row inside this plant's operator block (in bounds) and are replaced by the identity
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int gi = 4 * rb + i;
-            const double *row = ops + L.Ph + (size_t)(gi < n ? gi : n - 1) * n + 8 * cb;
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const int gj = 8 * cb + j;
-                const double v = row[j];
-                Mb[i][j] = (gi < n && gj < n) ? v : (gi == gj ? 1.0 : 0.0);
-            }
-        }
-    };
-    auto add_kkt = [&](double r) {  // + sigma I + r D SW[max(bi, bj)] D on the n x n part
-        double dj[8];
-        int bj[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int gj = 8 * cb + j;
-            dj[j] = s_D[gj];  // s_D is padded to kMimoN (1.0)
-            bj[j] = gj >> lognu;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int gi = 4 * rb + i;
-            const int bi = gi >> lognu, ci = gi & (nu - 1);
-            const double di = s_D[gi];
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const int gj = 8 * cb + j;
-                const int bm = bi > bj[j] ? bi : bj[j], cj = gj & (nu - 1);
-                const int bmc = bm < N ? bm : N - 1;
-                const double g = (di * dj[j]) * s_SW[(bmc * nu + ci) * nu + cj];
-                const double v = Mb[i][j] + (gi == gj ? sigma : 0.0) + r * g;
-                if (gi < n && gj < n) Mb[i][j] = v;
-            }
-        }
-    };
-    auto invert = [&]() {
-        for (int k = 0; k < n; k++) {
-            const int p = k & 1;
-            const int ik = k - 4 * rb, jk = k - 8 * cb;  // this thread's row / column of index k, if any
-            if (ik >= 0 && ik < 4)
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-                    if (i == ik)
-#pragma unroll
-                        for (int j = 0; j < 8; j++) s_row[p][8 * cb + j] = Mb[i][j];
-            if (jk >= 0 && jk < 8)
-#pragma unroll
-                for (int j = 0; j < 8; j++)
-                    if (j == jk)
-#pragma unroll
-                        for (int i = 0; i < 4; i++) s_col[p][4 * rb + i] = Mb[i][j];
-            __syncthreads();
-            const double piv = s_row[p][k];
-            if (!(piv > 0.0)) fail = 1;
-            const double inv = 1.0 / piv;
-            double rj[8], ci[4];
-            {
-                const double2 *r2 = (const double2 *)&s_row[p][8 * cb];
-                const double2 *c2 = (const double2 *)&s_col[p][4 * rb];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const double2 v = r2[j];
-                    rj[2 * j] = v.x;
-                    rj[2 * j + 1] = v.y;
-                }
-#pragma unroll
-                for (int i = 0; i < 2; i++) {
-                    const double2 v = c2[i];
-                    ci[2 * i] = v.x * inv;
-                    ci[2 * i + 1] = v.y * inv;
-                }
-            }
-            // a_ij -= (a_ik / a_kk) a_kj everywhere, then row k and column k are overwritten
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-#pragma unroll
-                for (int j = 0; j < 8; j++) Mb[i][j] = __builtin_fma(-ci[i], rj[j], Mb[i][j]);
-            if (jk >= 0 && jk < 8)
-#pragma unroll
-                for (int j = 0; j < 8; j++)
-                    if (j == jk)
-#pragma unroll
-                        for (int i = 0; i < 4; i++) Mb[i][j] = -ci[i];
-            if (ik >= 0 && ik < 4)
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-                    if (i == ik)
-#pragma unroll
-                        for (int j = 0; j < 8; j++) Mb[i][j] = (j == jk) ? inv : rj[j] * inv;
-        }
-    };
-    // ---- wave 0's vector kernels (element e = lane + 64 s; padding elements e >= n kept at 0)
-    auto vmask = [&](V2 v) {
-        for (int s = 0; s < 2; s++)
-            if (lane + 64 * s >= n) v.v[s] = 0.0;
+            for (int c = 0; c < 4; c++) v.v[c] = 0.0;
         return v;
     };
-    auto At_of = [&](V2 d) {  // A^' [w_top; w_bot] given d = w_top - w_bot (per element)
-        const V2 E = ld2(s_E), D = ld2(s_D);
-        V2 v;
-        for (int s = 0; s < 2; s++) v.v[s] = E.v[s] * d.v[s];
-        v = blk_suffix(vmask(v), nu, lane);
-        v = blk_k0(v, s_K0, nu, lane, true);
-        for (int s = 0; s < 2; s++) v.v[s] *= D.v[s];
-        return vmask(v);
+    auto k0_plain = [&](const B4 &x) {  // out[r] = sum_c K0[r][c] x[c]
+        B4 o;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            double acc = 0.0;
+#pragma unroll
+            for (int c = 0; c < NU; c++) acc = __builtin_fma(s_K0[r * 4 + c], x.v[c], acc);
+            o.v[r] = r < NU ? acc : 0.0;
+        }
+        return o;
     };
-    auto A_of = [&](V2 xv) {  // (A^ x)_top; the bottom half is its negation
-        const V2 E = ld2(s_E), D = ld2(s_D);
-        V2 v;
-        for (int s = 0; s < 2; s++) v.v[s] = D.v[s] * xv.v[s];
-        v = blk_prefix(vmask(v), nu, lane);
-        v = blk_k0(v, s_K0, nu, lane, false);
-        for (int s = 0; s < 2; s++) v.v[s] *= E.v[s];
-        return vmask(v);
+    auto k0_trans = [&](const B4 &x) {  // out[c] = sum_r K0[r][c] x[r]
+        B4 o;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            double acc = 0.0;
+#pragma unroll
+            for (int r = 0; r < NU; r++) acc = __builtin_fma(s_K0[r * 4 + c], x.v[r], acc);
+            o.v[c] = c < NU ? acc : 0.0;
+        }
+        return o;
     };
-    auto make_rhs = [&]() {  // s_vec = rhs = sigma x - q^ + A^'(rho z - y)
-        const V2 zt = ld2(s_zt), zb = ld2(s_zb), yt = ld2(s_yt), yb = ld2(s_yb), x = ld2(s_x), qh = ld2(s_qh);
-        V2 d;
-        for (int s = 0; s < 2; s++) d.v[s] = (rho * zt.v[s] - yt.v[s]) - (rho * zb.v[s] - yb.v[s]);
-        const V2 atw = At_of(d);
-        V2 r;
-        for (int s = 0; s < 2; s++) r.v[s] = (lane + 64 * s < n) ? (sigma * x.v[s] - qh.v[s]) + atw.v[s] : 0.0;
-        st2(s_vec, r);
+    auto A_of = [&](const B4 &xv) {  // (A^ x)_top = E (L (x) K0) D x; the bottom half is its negation
+        const B4 D = ldb(s_D, lane), E = ldb(s_E, lane);
+        B4 v;
+#pragma unroll
+        for (int c = 0; c < 4; c++) v.v[c] = c < NU ? lane_prefix(D.v[c] * xv.v[c], lane) : 0.0;
+        v = k0_plain(v);
+#pragma unroll
+        for (int c = 0; c < 4; c++) v.v[c] *= E.v[c];
+        return lmask(v);
+    };
+    // A^' [w_top; w_bot] = D (L (x) K0)' E d, d = w_top - w_bot; two right-hand sides in one pass
+    auto At_of2 = [&](const B4 &d1, const B4 &d2, B4 &o1, B4 &o2) {
+        const B4 D = ldb(s_D, lane), E = ldb(s_E, lane);
+        const B4 v1 = lmask(d1), v2 = lmask(d2);
+        B4 s1, s2;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            s1.v[c] = c < NU ? lane_suffix(E.v[c] * v1.v[c], lane) : 0.0;
+            s2.v[c] = c < NU ? lane_suffix(E.v[c] * v2.v[c], lane) : 0.0;
+        }
+        s1 = k0_trans(s1);
+        s2 = k0_trans(s2);
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            s1.v[c] *= D.v[c];
+            s2.v[c] *= D.v[c];
+        }
+        o1 = lmask(s1);
+        o2 = lmask(s2);
+    };
+    auto At_of = [&](const B4 &d) {
+        const B4 D = ldb(s_D, lane), E = ldb(s_E, lane);
+        B4 v = lmask(d);
+#pragma unroll
+        for (int c = 0; c < 4; c++) v.v[c] = c < NU ? lane_suffix(E.v[c] * v.v[c], lane) : 0.0;
+        v = k0_trans(v);
+#pragma unroll
+        for (int c = 0; c < 4; c++) v.v[c] *= D.v[c];
+        return lmask(v);
+    };
+    auto ld_nat = [&](const double *arr) {  // natural-order vector -> this lane's block
+        B4 v;
+        const int kk = lane < N ? lane : 0;
+#pragma unroll
+        for (int c = 0; c < 4; c++) v.v[c] = (c < NU && lane < N) ? arr[kk * NU + (c < NU ? c : 0)] : 0.0;
+        return v;
+    };
+    auto st_rhs = [&](const B4 &r) {  // rhs to s_vec (natural, GEMV input) and s_rhs (block-major)
+        stb(s_rhs, lane, r);
+        if (lane < N)
+#pragma unroll
+            for (int c = 0; c < NU; c++) s_vec[lane * NU + c] = r.v[c];
+    };
+    auto make_rhs = [&]() {  // rhs = sigma x - q^ + A^'(rho z - y)
+        const B4 zt = ldb(s_zt, lane), zb = ldb(s_zb, lane), yt = ldb(s_yt, lane), yb = ldb(s_yb, lane);
+        B4 d;
+#pragma unroll
+        for (int c = 0; c < 4; c++) d.v[c] = (rho * zt.v[c] - yt.v[c]) - (rho * zb.v[c] - yb.v[c]);
+        const B4 atw = At_of(d);
+        const B4 x = ldb(s_x, lane), qh = ldb(s_qh, lane);
+        B4 r;
+#pragma unroll
+        for (int c = 0; c < 4; c++) r.v[c] = (sigma * x.v[c] - qh.v[c]) + atw.v[c];
+        st_rhs(lmask(r));
     };
 
     const int ct = st.check_termination;
     const int ai = (st.adaptive_rho && a.adaptive_interval) ? a.adaptive_interval : 0;
-    int it = 0;
+    int it = 0, nfact = 0;
     int next_check = ct ? ct : -1, next_adapt = ai ? ai : -1;
+    bool px_pending = load;  // warm start: the first phase takes P^ x from s_nat
 
-    auto finalize = [&]() {  // wave 0: OSQP store_solution + the MPC front end's U += x[0:nu] (:105)
+    auto finalize = [&]() {  // OSQP store_solution + the MPC front end's U += x[0:nu] (:105)
         const bool has_sol = status == kSolved || status == kSolvedInaccurate || status == kMaxIterReached;
         const bool keep = has_sol || status == kInvalidBounds || status == kTypeChanged;
-        for (int s = 0; s < 2; s++) {
-            const int e = lane + 64 * s;
-            if (e >= n) continue;
-            const double x = s_x[e], zt = s_zt[e], zb = s_zb[e], yt = s_yt[e], yb = s_yb[e], Ee = s_E[e];
-            const double xv = has_sol ? x * s_D[e] : __builtin_nan("");
-            if (a.x) a.x[(size_t)b * n + e] = xv;
-            if (a.y) {
-                a.y[(size_t)b * m + e] = has_sol ? (yt * Ee) * cinv : __builtin_nan("");
-                a.y[(size_t)b * m + n + e] = has_sol ? (yb * Ee) * cinv : __builtin_nan("");
+        const B4 x = ldb(s_x, lane), zt = ldb(s_zt, lane), zb = ldb(s_zb, lane), yt = ldb(s_yt, lane);
+        const B4 yb = ldb(s_yb, lane), D = ldb(s_D, lane), E = ldb(s_E, lane);
+        if (lane < N) {
+#pragma unroll
+            for (int c = 0; c < NU; c++) {
+                const int e = lane * NU + c;
+                const double xv = has_sol ? x.v[c] * D.v[c] : __builtin_nan("");
+                if (a.x) a.x[(size_t)b * n + e] = xv;
+                if (a.y) {
+                    a.y[(size_t)b * m + e] = has_sol ? (yt.v[c] * E.v[c]) * cinv : __builtin_nan("");
+                    a.y[(size_t)b * m + n + e] = has_sol ? (yb.v[c] * E.v[c]) * cinv : __builtin_nan("");
+                }
+                if (lane == 0 && status == kSolved) a.U[(size_t)b * NU + c] = a.U[(size_t)b * NU + c] + xv;
+                a.xs[(size_t)b * n + e] = keep ? x.v[c] : 0.0;
+                a.zs[(size_t)b * m + e] = keep ? zt.v[c] : 0.0;
+                a.zs[(size_t)b * m + n + e] = keep ? zb.v[c] : 0.0;
+                a.ys[(size_t)b * m + e] = keep ? yt.v[c] : 0.0;
+                a.ys[(size_t)b * m + n + e] = keep ? yb.v[c] : 0.0;
             }
-            if (e < nu && status == kSolved) a.U[(size_t)b * nu + e] = a.U[(size_t)b * nu + e] + xv;
-            a.xs[(size_t)b * n + e] = keep ? x : 0.0;
-            a.zs[(size_t)b * m + e] = keep ? zt : 0.0;
-            a.zs[(size_t)b * m + n + e] = keep ? zb : 0.0;
-            a.ys[(size_t)b * m + e] = keep ? yt : 0.0;
-            a.ys[(size_t)b * m + n + e] = keep ? yb : 0.0;
         }
         if (lane == 0) {
             a.rhos[b] = rho;
@@ -662,222 +800,277 @@ __global__ __launch_bounds__(kMimoThreads, 2) void mimo_solve_kernel(MimoArgs a)
         }
     };
 
-    // control word (s_ctrl[0]): 0 continue, 1 (re-)invert M(s_rho) then continue, 2 done.  The first
-    // factorisation takes the same path (s_ctrl[1]: also form P^ x of a warm start).
-    if (wv == 0) {
-        if (status != kUnsolved) {
-            finalize();
-            if (lane == 0) s_ctrl[0] = 2;
-        } else {
-            make_rhs();
-            if (lane == 0) s_ctrl[0] = 1;
-        }
+    // control word (s_ctrl[0]): 0 continue, 1 (re-)invert M(s_rho) then continue, 2 done
+    if (status != kUnsolved) {
+        finalize();
+    } else {
+        make_rhs();
+    }
+    if (lane == 0) {
+        s_rho = rho;
+        s_ctrl[0] = status != kUnsolved ? 2 : 1;
+        s_ctrl[1] = load ? 1 : 0;
     }
     __syncthreads();
     for (;;) {
         const int ctrl = s_ctrl[0];
         if (ctrl == 2) break;
         if (ctrl == 1) {
-            load_P();
-            if (s_ctrl[1]) {  // warm start: P^ x of the loaded x (s_x holds it; s_px receives)
-                gemv(s_x, s_px);
+            if (s_ctrl[1]) {
                 __syncthreads();
-                if (t == 0) s_ctrl[1] = 0;
+                __syncthreads();
             }
-            add_kkt(s_rho);
-            invert();  // its first barrier orders wave 0's s_vec writes before the GEMV below
+            for (int k = 0; k < n; k++) {  // the matrix waves' Gauss-Jordan steps
+                __syncthreads();
+                if (!(s_row[k & 1][k] > 0.0)) fail = 1;
+            }
+            nfact++;
             if (fail) {  // P^ + sigma I + rho A^'A^ not positive definite
-                if (wv == 0) {
-                    status = kNonCvx;
-                    finalize();
-                }
+                status = kNonCvx;
+                finalize();
                 break;
             }
         }
-        gemv(s_vec, s_out);
-        __syncthreads();
-        if (wv == 0) {
-            it++;
-            const bool at_check = it == next_check, at_adapt = it == next_adapt;
-            if (at_check) next_check += ct;
-            if (at_adapt) next_adapt += ai;
-            const bool last = it == st.max_iter;
-            const bool info = at_check || at_adapt || last;
-            const double rinv = 1.0 / rho;
-            // ---- x~ = M^-1 rhs ; z~ = A^ x~ ; P^ x~ = rhs - sigma x~ - rho A^'z~ ; relax ; project ; dual
-            V2 xt = vmask(ld2(s_out));
-            const V2 ztl = A_of(xt);
-            V2 d2;
-            for (int s = 0; s < 2; s++) d2.v[s] = 2.0 * ztl.v[s];
-            const V2 gz = At_of(d2);
-            const V2 rhs = ld2(s_vec);
-            V2 x = ld2(s_x), px = ld2(s_px), zt = ld2(s_zt), zb = ld2(s_zb), yt = ld2(s_yt), yb = ld2(s_yb);
-            const V2 ut = ld2(s_ut), ub = ld2(s_ub);
-            V2 dx, dpx, dyt, dyb;
-            for (int s = 0; s < 2; s++) {
-                const double ptx = (rhs.v[s] - sigma * xt.v[s]) - rho * gz.v[s];
-                const double pxn = __builtin_fma(alpha, ptx, oma * px.v[s]);
-                const double xn = __builtin_fma(alpha, xt.v[s], oma * x.v[s]);
-                dx.v[s] = xn - x.v[s];
-                dpx.v[s] = pxn - px.v[s];
-                x.v[s] = xn;
-                px.v[s] = pxn;
-                // top row e and bottom row n + e (z~_bot = -z~_top)
-                const double vt = __builtin_fma(alpha, ztl.v[s], oma * zt.v[s]);
-                const double zn_t = fmin(__builtin_fma(rinv, yt.v[s], vt), ut.v[s]);
-                dyt.v[s] = rho * (vt - zn_t);
-                yt.v[s] = __builtin_fma(rho, vt - zn_t, yt.v[s]);
-                zt.v[s] = zn_t;
-                const double vb = __builtin_fma(alpha, -ztl.v[s], oma * zb.v[s]);
-                const double zn_b = fmin(__builtin_fma(rinv, yb.v[s], vb), ub.v[s]);
-                dyb.v[s] = rho * (vb - zn_b);
-                yb.v[s] = __builtin_fma(rho, vb - zn_b, yb.v[s]);
-                zb.v[s] = zn_b;
+        __syncthreads();  // x~ ready
+        it++;
+        const bool at_check = it == next_check, at_adapt = it == next_adapt;
+        if (at_check) next_check += ct;
+        if (at_adapt) next_adapt += ai;
+        const bool last = it == st.max_iter;
+        const bool info = at_check || at_adapt || last;
+        const double rinv = 1.0 / rho;
+        // ---- x~ = M^-1 rhs ; z~ = A^ x~ ; P^ x~ = rhs - sigma x~ - rho A^'z~ ; relax ; project ; dual
+        const B4 xt = ld_nat(s_out);
+        const B4 ztl = A_of(xt);
+        B4 d2, dr;
+        {  // x: relaxation
+            const B4 x = ldb(s_x, lane);
+            B4 xn, dx;
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                xn.v[c] = __builtin_fma(alpha, xt.v[c], oma * x.v[c]);
+                dx.v[c] = xn.v[c] - x.v[c];
             }
-            x = vmask(x); px = vmask(px); zt = vmask(zt); zb = vmask(zb); yt = vmask(yt); yb = vmask(yb);
-            dx = vmask(dx); dpx = vmask(dpx); dyt = vmask(dyt); dyb = vmask(dyb);
-            st2(s_x, x); st2(s_px, px); st2(s_zt, zt); st2(s_zb, zb); st2(s_yt, yt); st2(s_yb, yb);
-            int ctl = 0;
-            if (info) {
-                // ---- update_info: residuals (scaled norms _r, unscaled _s as OSQP reports them)
-                const V2 qh = ld2(s_qh), D = ld2(s_D), E = ld2(s_E);
-                const V2 ax = A_of(x);
-                V2 dy;
-                for (int s = 0; s < 2; s++) dy.v[s] = yt.v[s] - yb.v[s];
-                const V2 aty = At_of(dy);
-                double ax_z = 0, ax_zs = 0, zn_r = 0, zn_s = 0, axn_r = 0, axn_s = 0;
-                double dr_r = 0, dr_s = 0, qn_r = 0, qn_s = 0, atyn_r = 0, atyn_s = 0, pxn_r = 0, pxn_s = 0;
-                for (int s = 0; s < 2; s++) {
-                    if (lane + 64 * s >= n) continue;
-                    const double ei = 1.0 / E.v[s], di = 1.0 / D.v[s];
-                    const double rt = ax.v[s] - zt.v[s], rbm = -ax.v[s] - zb.v[s];
-                    ax_z = fmax(ax_z, fmax(fabs(rt), fabs(rbm)));
-                    ax_zs = fmax(ax_zs, fmax(fabs(ei * rt), fabs(ei * rbm)));
-                    zn_r = fmax(zn_r, fmax(fabs(zt.v[s]), fabs(zb.v[s])));
-                    zn_s = fmax(zn_s, fmax(fabs(ei * zt.v[s]), fabs(ei * zb.v[s])));
-                    axn_r = fmax(axn_r, fabs(ax.v[s]));
-                    axn_s = fmax(axn_s, fabs(ei * ax.v[s]));
-                    const double r = (qh.v[s] + px.v[s]) + aty.v[s];
-                    dr_r = fmax(dr_r, fabs(r));
-                    dr_s = fmax(dr_s, fabs(di * r));
-                    qn_r = fmax(qn_r, fabs(qh.v[s]));
-                    qn_s = fmax(qn_s, fabs(di * qh.v[s]));
-                    atyn_r = fmax(atyn_r, fabs(aty.v[s]));
-                    atyn_s = fmax(atyn_s, fabs(di * aty.v[s]));
-                    pxn_r = fmax(pxn_r, fabs(px.v[s]));
-                    pxn_s = fmax(pxn_s, fabs(di * px.v[s]));
+            stb(s_x, lane, lmask(xn));
+            stb(s_dx, lane, lmask(dx));
+        }
+        {  // z, y: top row e and bottom row n + e (z~_bot = -z~_top)
+            B4 zt = ldb(s_zt, lane), zb = ldb(s_zb, lane), yt = ldb(s_yt, lane), yb = ldb(s_yb, lane);
+            const B4 ut = ldb(s_ut, lane), ub = ldb(s_ub, lane);
+            B4 dyt, dyb;
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const double vt = __builtin_fma(alpha, ztl.v[c], oma * zt.v[c]);
+                const double zn_t = fmin(__builtin_fma(rinv, yt.v[c], vt), ut.v[c]);
+                dyt.v[c] = rho * (vt - zn_t);
+                yt.v[c] = __builtin_fma(rho, vt - zn_t, yt.v[c]);
+                zt.v[c] = zn_t;
+                const double vb = __builtin_fma(alpha, -ztl.v[c], oma * zb.v[c]);
+                const double zn_b = fmin(__builtin_fma(rinv, yb.v[c], vb), ub.v[c]);
+                dyb.v[c] = rho * (vb - zn_b);
+                yb.v[c] = __builtin_fma(rho, vb - zn_b, yb.v[c]);
+                zb.v[c] = zn_b;
+                d2.v[c] = 2.0 * ztl.v[c];
+                dr.v[c] = (rho * zt.v[c] - yt.v[c]) - (rho * zb.v[c] - yb.v[c]);  // next rhs (rho unchanged)
+            }
+            stb(s_zt, lane, lmask(zt)); stb(s_zb, lane, lmask(zb)); stb(s_yt, lane, lmask(yt)); stb(s_yb, lane, lmask(yb));
+            stb(s_dyt, lane, lmask(dyt)); stb(s_dyb, lane, lmask(dyb));
+        }
+        B4 gz, atw;
+        if (info)
+            gz = At_of(d2);
+        else
+            At_of2(d2, dr, gz, atw);
+        {  // carried P^ x (KKT identity)
+            const B4 rhs = ldb(s_rhs, lane);
+            B4 px = px_pending ? ld_nat(s_nat) : ldb(s_px, lane);
+            px_pending = false;
+            B4 dpx;
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const double ptx = (rhs.v[c] - sigma * xt.v[c]) - rho * gz.v[c];
+                const double pxn = __builtin_fma(alpha, ptx, oma * px.v[c]);
+                dpx.v[c] = pxn - px.v[c];
+                px.v[c] = pxn;
+            }
+            stb(s_px, lane, lmask(px));
+            stb(s_dpx, lane, lmask(dpx));
+        }
+        asm volatile("" ::: "memory");  // the stages below re-read the state (short register live ranges)
+        int ctl = 0;
+        if (info) {
+            // ---- update_info: residuals (scaled norms _r, unscaled _s as OSQP reports them)
+            double ax_z = 0, ax_zs = 0, zn_r = 0, zn_s = 0, axn_r = 0, axn_s = 0;
+            double dr_r = 0, dr_s = 0, qn_r = 0, qn_s = 0, atyn_r = 0, atyn_s = 0, pxn_r = 0, pxn_s = 0;
+            {
+                const B4 ax = A_of(ldb(s_x, lane));
+                const B4 zt = ldb(s_zt, lane), zb = ldb(s_zb, lane), E = ldb(s_E, lane);
+                if (lane < N) {
+#pragma unroll
+                    for (int c = 0; c < NU; c++) {
+                        const double ei = 1.0 / E.v[c];
+                        const double rt = ax.v[c] - zt.v[c], rbm = -ax.v[c] - zb.v[c];
+                        ax_z = fmax(ax_z, fmax(fabs(rt), fabs(rbm)));
+                        ax_zs = fmax(ax_zs, fmax(fabs(ei * rt), fabs(ei * rbm)));
+                        zn_r = fmax(zn_r, fmax(fabs(zt.v[c]), fabs(zb.v[c])));
+                        zn_s = fmax(zn_s, fmax(fabs(ei * zt.v[c]), fabs(ei * zb.v[c])));
+                        axn_r = fmax(axn_r, fabs(ax.v[c]));
+                        axn_s = fmax(axn_s, fabs(ei * ax.v[c]));
+                    }
                 }
-                ax_z = wmax(ax_z); ax_zs = wmax(ax_zs); zn_r = wmax(zn_r); zn_s = wmax(zn_s);
-                axn_r = wmax(axn_r); axn_s = wmax(axn_s); dr_r = wmax(dr_r); dr_s = wmax(dr_s);
-                qn_r = wmax(qn_r); qn_s = wmax(qn_s); atyn_r = wmax(atyn_r); atyn_s = wmax(atyn_s);
-                pxn_r = wmax(pxn_r); pxn_s = wmax(pxn_s);
-                const bool scaled_term = st.scaled_termination != 0;
-                const double pri_res = scaled_term ? ax_z : ax_zs;
-                const double dua_res = scaled_term ? dr_r : cinv * dr_s;
+            }
+            {
+                const B4 yt = ldb(s_yt, lane), yb = ldb(s_yb, lane);
+                B4 dy;
+#pragma unroll
+                for (int c = 0; c < 4; c++) dy.v[c] = yt.v[c] - yb.v[c];
+                const B4 aty = At_of(dy);
+                const B4 qh = ldb(s_qh, lane), px = ldb(s_px, lane), D = ldb(s_D, lane);
+                if (lane < N) {
+#pragma unroll
+                    for (int c = 0; c < NU; c++) {
+                        const double di = 1.0 / D.v[c];
+                        const double r = (qh.v[c] + px.v[c]) + aty.v[c];
+                        dr_r = fmax(dr_r, fabs(r));
+                        dr_s = fmax(dr_s, fabs(di * r));
+                        qn_r = fmax(qn_r, fabs(qh.v[c]));
+                        qn_s = fmax(qn_s, fabs(di * qh.v[c]));
+                        atyn_r = fmax(atyn_r, fabs(aty.v[c]));
+                        atyn_s = fmax(atyn_s, fabs(di * aty.v[c]));
+                        pxn_r = fmax(pxn_r, fabs(px.v[c]));
+                        pxn_s = fmax(pxn_s, fabs(di * px.v[c]));
+                    }
+                }
+            }
+            ax_z = wmax(ax_z); ax_zs = wmax(ax_zs); zn_r = wmax(zn_r); zn_s = wmax(zn_s);
+            axn_r = wmax(axn_r); axn_s = wmax(axn_s); dr_r = wmax(dr_r); dr_s = wmax(dr_s);
+            qn_r = wmax(qn_r); qn_s = wmax(qn_s); atyn_r = wmax(atyn_r); atyn_s = wmax(atyn_s);
+            pxn_r = wmax(pxn_r); pxn_s = wmax(pxn_s);
+            const bool scaled_term = st.scaled_termination != 0;
+            const double pri_res = scaled_term ? ax_z : ax_zs;
+            const double dua_res = scaled_term ? dr_r : cinv * dr_s;
 
-                // OSQP is_primal_infeasible on delta_y (u finite, l = -inf on every row: d = max(d, 0))
-                auto primal_inf = [&](double eps) -> bool {
-                    double ndy = 0.0, lhs = 0.0;
-                    V2 dd;
-                    for (int s = 0; s < 2; s++) {
-                        const double dt_ = fmax(dyt.v[s], 0.0), db_ = fmax(dyb.v[s], 0.0);
-                        dd.v[s] = dt_ - db_;
-                        if (lane + 64 * s < n) {
-                            ndy = fmax(ndy, fmax(fabs(scaled_term ? dt_ : E.v[s] * dt_), fabs(scaled_term ? db_ : E.v[s] * db_)));
-                            lhs += ut.v[s] * dt_;
-                            lhs += ub.v[s] * db_;
-                        }
-                    }
-                    ndy = wmax(ndy);
-                    lhs = wsum(lhs);
-                    if (!(ndy > kDivisionTol && lhs < eps * ndy)) return false;
-                    const V2 atd = At_of(dd);
-                    double nat = 0.0;
-                    for (int s = 0; s < 2; s++)
-                        if (lane + 64 * s < n) nat = fmax(nat, fabs(scaled_term ? atd.v[s] : atd.v[s] / D.v[s]));
-                    nat = wmax(nat);
-                    return nat < eps * ndy;
-                };
-                // OSQP is_dual_infeasible on delta_x (P^ delta_x = delta of the carried P^ x)
-                auto dual_inf = [&](double eps) -> bool {
-                    double qdx = 0.0, ndx = 0.0;
-                    for (int s = 0; s < 2; s++)
-                        if (lane + 64 * s < n) {
-                            qdx = __builtin_fma(qh.v[s], dx.v[s], qdx);
-                            ndx = fmax(ndx, fabs(scaled_term ? dx.v[s] : D.v[s] * dx.v[s]));
-                        }
-                    qdx = wsum(qdx);
-                    ndx = wmax(ndx);
-                    const double cs = scaled_term ? 1.0 : c64;
-                    if (!(qdx < 0.0 && ndx > kDivisionTol && qdx < -cs * eps * ndx)) return false;
-                    double npdx = 0.0;
-                    for (int s = 0; s < 2; s++)
-                        if (lane + 64 * s < n) npdx = fmax(npdx, fabs(scaled_term ? dpx.v[s] : dpx.v[s] / D.v[s]));
-                    npdx = wmax(npdx);
-                    if (!(npdx < cs * eps * ndx)) return false;
-                    const V2 adx = A_of(dx);
-                    int viol = 0;
-                    for (int s = 0; s < 2; s++)
-                        if (lane + 64 * s < n) {
-                            const double sv = scaled_term ? adx.v[s] : adx.v[s] / E.v[s];
-                            if (ut.v[s] < kInfty * kMinScaling && sv > eps * ndx) viol = 1;   // top row
-                            if (ub.v[s] < kInfty * kMinScaling && -sv > eps * ndx) viol = 1;  // bottom row
-                        }
-                    return !wave_any(viol != 0);
-                };
-                auto check = [&](bool approx) -> int {
-                    const double mul = approx ? 10.0 : 1.0;
-                    const double ea = st.eps_abs * mul, er = st.eps_rel * mul;
-                    if (pri_res > kInfty || dua_res > kInfty) return kNonCvx;
-                    const double ep = ea + er * (scaled_term ? fmax(zn_r, axn_r) : fmax(zn_s, axn_s));
-                    const double ed = ea + er * (scaled_term ? fmax(fmax(qn_r, atyn_r), pxn_r)
-                                                             : cinv * fmax(fmax(qn_s, atyn_s), pxn_s));
-                    const bool pok = pri_res < ep, dok = dua_res < ed;
-                    if (pok && dok) return approx ? kSolvedInaccurate : kSolved;
-                    if (!pok && primal_inf(st.eps_prim_inf * mul))
-                        return approx ? kPrimalInfeasibleInaccurate : kPrimalInfeasible;
-                    if (!dok && dual_inf(st.eps_dual_inf * mul))
-                        return approx ? kDualInfeasibleInaccurate : kDualInfeasible;
-                    return kUnsolved;
-                };
-                // OSQP order: check at check iterations, adapt_rho at adapt iterations, and after the last
-                // iteration an exact then an approximate check (osqp_solve); one call site for check()
-                for (int pass = 0; pass < 2; pass++) {
-                    if (status != kUnsolved) break;
-                    if (pass == 0) {
-                        if (at_check || last) status = check(false);
-                        if (status == kUnsolved && at_adapt && !last) {  // adapt_rho (scaled norms)
-                            const double pr = ax_z / (fmax(zn_r, axn_r) + kDivisionTol);
-                            const double dn = fmax(fmax(qn_r, atyn_r), pxn_r);
-                            const double du = dr_r / (dn + kDivisionTol);
-                            double rn = rho * sqrt(pr / (du + kDivisionTol));
-                            rn = fmin(fmax(rn, kRhoMin), kRhoMax);
-                            if (rn > rho * st.adaptive_rho_tolerance || rn < rho / st.adaptive_rho_tolerance) {
-                                rho = fmin(fmax(rn, kRhoMin), kRhoMax);
-                                ctl = 1;
-                            }
-                        }
-                    } else if (last) {
-                        const int s2 = check(true);
-                        status = s2 != kUnsolved ? s2 : kMaxIterReached;
+            // OSQP is_primal_infeasible on delta_y (u finite, l = -inf on every row: d = max(d, 0))
+            auto primal_inf = [&](double eps) -> bool {
+                const B4 dyt = ldb(s_dyt, lane), dyb = ldb(s_dyb, lane), ut = ldb(s_ut, lane), ub = ldb(s_ub, lane);
+                const B4 E = ldb(s_E, lane), D = ldb(s_D, lane);
+                double ndy = 0.0, lhs = 0.0;
+                B4 dd;
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const double dt_ = fmax(dyt.v[c], 0.0), db_ = fmax(dyb.v[c], 0.0);
+                    dd.v[c] = dt_ - db_;
+                    if (lane < N && c < NU) {
+                        ndy = fmax(ndy, fmax(fabs(scaled_term ? dt_ : E.v[c] * dt_), fabs(scaled_term ? db_ : E.v[c] * db_)));
+                        lhs += ut.v[c] * dt_;
+                        lhs += ub.v[c] * db_;
                     }
                 }
+                ndy = wmax(ndy);
+                lhs = wsum(lhs);
+                if (!(ndy > kDivisionTol && lhs < eps * ndy)) return false;
+                const B4 atd = At_of(dd);
+                double nat = 0.0;
+#pragma unroll
+                for (int c = 0; c < NU; c++)
+                    if (lane < N) nat = fmax(nat, fabs(scaled_term ? atd.v[c] : atd.v[c] / D.v[c]));
+                nat = wmax(nat);
+                return nat < eps * ndy;
+            };
+            // OSQP is_dual_infeasible on delta_x (P^ delta_x = delta of the carried P^ x)
+            auto dual_inf = [&](double eps) -> bool {
+                const B4 dx = ldb(s_dx, lane), qh = ldb(s_qh, lane), D = ldb(s_D, lane);
+                double qdx = 0.0, ndx = 0.0;
+#pragma unroll
+                for (int c = 0; c < NU; c++)
+                    if (lane < N) {
+                        qdx = __builtin_fma(qh.v[c], dx.v[c], qdx);
+                        ndx = fmax(ndx, fabs(scaled_term ? dx.v[c] : D.v[c] * dx.v[c]));
+                    }
+                qdx = wsum(qdx);
+                ndx = wmax(ndx);
+                const double cs = scaled_term ? 1.0 : c64;
+                if (!(qdx < 0.0 && ndx > kDivisionTol && qdx < -cs * eps * ndx)) return false;
+                double npdx = 0.0;
+                const B4 dpx = ldb(s_dpx, lane);
+#pragma unroll
+                for (int c = 0; c < NU; c++)
+                    if (lane < N) npdx = fmax(npdx, fabs(scaled_term ? dpx.v[c] : dpx.v[c] / D.v[c]));
+                npdx = wmax(npdx);
+                if (!(npdx < cs * eps * ndx)) return false;
+                const B4 adx = A_of(dx);
+                const B4 ut = ldb(s_ut, lane), ub = ldb(s_ub, lane), E = ldb(s_E, lane);
+                int viol = 0;
+#pragma unroll
+                for (int c = 0; c < NU; c++)
+                    if (lane < N) {
+                        const double sv = scaled_term ? adx.v[c] : adx.v[c] / E.v[c];
+                        if (ut.v[c] < kInfty * kMinScaling && sv > eps * ndx) viol = 1;   // top row
+                        if (ub.v[c] < kInfty * kMinScaling && -sv > eps * ndx) viol = 1;  // bottom row
+                    }
+                return !wave_any(viol != 0);
+            };
+            auto check = [&](bool approx) -> int {
+                const double mul = approx ? 10.0 : 1.0;
+                const double ea = st.eps_abs * mul, er = st.eps_rel * mul;
+                if (pri_res > kInfty || dua_res > kInfty) return kNonCvx;
+                const double ep = ea + er * (scaled_term ? fmax(zn_r, axn_r) : fmax(zn_s, axn_s));
+                const double ed = ea + er * (scaled_term ? fmax(fmax(qn_r, atyn_r), pxn_r)
+                                                         : cinv * fmax(fmax(qn_s, atyn_s), pxn_s));
+                const bool pok = pri_res < ep, dok = dua_res < ed;
+                if (pok && dok) return approx ? kSolvedInaccurate : kSolved;
+                if (!pok && primal_inf(st.eps_prim_inf * mul))
+                    return approx ? kPrimalInfeasibleInaccurate : kPrimalInfeasible;
+                if (!dok && dual_inf(st.eps_dual_inf * mul))
+                    return approx ? kDualInfeasibleInaccurate : kDualInfeasible;
+                return kUnsolved;
+            };
+            // OSQP order: check at check iterations, adapt_rho at adapt iterations, and after the last
+            // iteration an exact then an approximate check (osqp_solve); one call site for check()
+            for (int pass = 0; pass < 2; pass++) {
+                if (status != kUnsolved) break;
+                if (pass == 0) {
+                    if (at_check || last) status = check(false);
+                    if (status == kUnsolved && at_adapt && !last) {  // adapt_rho (scaled norms)
+                        const double pr = ax_z / (fmax(zn_r, axn_r) + kDivisionTol);
+                        const double dn = fmax(fmax(qn_r, atyn_r), pxn_r);
+                        const double du = dr_r / (dn + kDivisionTol);
+                        double rn = rho * sqrt(pr / (du + kDivisionTol));
+                        rn = fmin(fmax(rn, kRhoMin), kRhoMax);
+                        if (rn > rho * st.adaptive_rho_tolerance || rn < rho / st.adaptive_rho_tolerance) {
+                            rho = fmin(fmax(rn, kRhoMin), kRhoMax);
+                            ctl = 1;
+                        }
+                    }
+                } else if (last) {
+                    const int s2 = check(true);
+                    status = s2 != kUnsolved ? s2 : kMaxIterReached;
+                }
             }
-            if (status != kUnsolved) {
-                finalize();
-                ctl = 2;
-            } else {
-                make_rhs();
-            }
-            if (lane == 0) {
-                s_ctrl[0] = ctl;
-                s_rho = rho;
-            }
+        }
+        if (status != kUnsolved) {
+            finalize();
+            ctl = 2;
+        } else if (info) {
+            make_rhs();  // rho may have changed
+        } else {
+            const B4 qh = ldb(s_qh, lane), x = ldb(s_x, lane);
+            B4 r;
+#pragma unroll
+            for (int c = 0; c < 4; c++) r.v[c] = (sigma * x.v[c] - qh.v[c]) + atw.v[c];
+            st_rhs(lmask(r));
+        }
+        if (lane == 0) {
+            s_ctrl[0] = ctl;
+            s_rho = rho;
         }
         __syncthreads();
     }
-    MPCQ_MSTAMP(3, __builtin_amdgcn_s_memtime());
-    MPCQ_MSTAMP(4, it);
+    if (a.stamps && lane == 0) {
+        a.stamps[(size_t)blockIdx.x * 8 + 3] = (long long)__builtin_amdgcn_s_memtime();
+        a.stamps[(size_t)blockIdx.x * 8 + 4] = it;
+        a.stamps[(size_t)blockIdx.x * 8 + 5] = nfact;
+    }
 }
 
 }  // namespace mpcq
@@ -899,8 +1092,13 @@ extern "C" int mpcq_internal_mimo_setup_launch(const mpcq::MimoSetupArgs *a, hip
 
 extern "C" int mpcq_internal_mimo_solve_launch(const mpcq::MimoArgs *a, hipStream_t s)
 {
-    if (a->nx > 12 || a->nu > 4 || 64 % a->nu != 0 || a->ny > 12 || a->N * a->nu > mpcq::kMimoN || a->N > 32)
-        return -1;
-    hipLaunchKernelGGL(mpcq::mimo_solve_kernel, dim3(a->batch), dim3(mpcq::kMimoThreads), 0, s, *a);
+    if (a->nx > 12 || a->ny > 12 || a->N * a->nu > mpcq::kMimoN || a->N > 32) return -1;
+    const dim3 grid(a->batch), block(mpcq::kMimoThreads);
+    switch (a->nu) {
+    case 1: hipLaunchKernelGGL(mpcq::mimo_solve_kernel<1>, grid, block, 0, s, *a); break;
+    case 2: hipLaunchKernelGGL(mpcq::mimo_solve_kernel<2>, grid, block, 0, s, *a); break;
+    case 4: hipLaunchKernelGGL(mpcq::mimo_solve_kernel<4>, grid, block, 0, s, *a); break;
+    default: return -1;
+    }
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
