@@ -1064,12 +1064,29 @@ int mpcq_mimo_setup_plants_device(mpcq_ctx *c, int nx, int nu, int ny, int s_row
     a.Ad = Ad; a.Bd = Bd; a.Cd = Cd; a.Q = Q; a.R = R; a.RD = RD; a.K = K; a.K0 = K0; a.w0 = w0;
     a.ops = c->d_mimo;
     a.flags = c->d_flags;
+    const char *sst = std::getenv("MPCQ_MIMO_SETUP_STAMPS");  // debug hook: per-plant phase stamps
+    if (sst && *sst) {
+        if (c->d_stamps) (void)hipFree(c->d_stamps);
+        if (hipMalloc((void **)&c->d_stamps, 8 * 16 * (size_t)a.n_plants) != hipSuccess)
+            return fail(MPCQ_ERR_HIP, "hipMalloc failed (stamps)");
+        a.stamps = c->d_stamps;
+    }
     const int lr = mpcq_internal_mimo_setup_launch(&a, s);
     if (lr == -1) return fail(MPCQ_ERR_ARG, "mimo: shape beyond the setup kernel's LDS capacity");
     if (lr) return fail(MPCQ_ERR_HIP, std::string("mimo setup launch failed: ") + hipGetErrorString(hipGetLastError()));
     int flags = 0;
     HIPCHK(hipMemcpyAsync(&flags, c->d_flags, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    if (sst && *sst) {
+        std::vector<long long> h(16 * (size_t)a.n_plants);
+        HIPCHK(hipMemcpy(h.data(), c->d_stamps, 8 * h.size(), hipMemcpyDeviceToHost));
+        (void)hipFree(c->d_stamps);
+        c->d_stamps = nullptr;
+        if (FILE *f = std::fopen(sst, "wb")) {
+            std::fwrite(h.data(), 8, h.size(), f);
+            std::fclose(f);
+        }
+    }
     if (flags & 2) return fail(MPCQ_ERR_SETUP, "mimo: a constraint row is not an inequality (|w0| beyond OSQP_INFTY)");
     c->last = s;
     c->fresh = true;  // the first step starts from x = z = y = 0, rho = settings.rho (initSolver, :64)

@@ -54,7 +54,13 @@ def run(label, stamps=None, **over):
     s.close()
 
 
+if len(sys.argv) > 2 and sys.argv[2] == "setup":
+    os.environ["MPCQ_MIMO_SETUP_STAMPS"] = "gpurun_out/setup_stamps.bin"
+    run("setup stamps", max_iter=1, adaptive_rho=0)
+    sys.exit(0)
 run("max_iter 1, no adapt", max_iter=1, adaptive_rho=0, stamps="gpurun_out/ms1.bin")
+if len(sys.argv) > 2 and sys.argv[2] == "gj":
+    sys.exit(0)
 run("max_iter 25, no adapt", max_iter=25, adaptive_rho=0, stamps="gpurun_out/ms25.bin")
 run("max_iter 100, no adapt", max_iter=100, adaptive_rho=0, check_termination=0)
 run("default", stamps="gpurun_out/msd.bin")
