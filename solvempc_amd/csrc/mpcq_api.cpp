@@ -83,7 +83,7 @@ struct mpcq_ctx {
              unsigned long long gen; } gkey{};
     // MIMO condensed MPC (mpcq_mimo.hip): per-plant operator block, dims
     double *d_mimo = nullptr;
-    int mimo_N = 0, mimo_nx = 0, mimo_nu = 0, mimo_ny = 0, mimo_srows = 0;
+    int mimo_N = 0, mimo_nx = 0, mimo_nu = 0, mimo_ny = 0, mimo_srows = 0, mimo_diag_k0 = 0;
     bool mimo_ready = false, mimo_only = false;
     // host copies of plant-0 scaling
     std::vector<double> hD, hE;
@@ -1088,6 +1088,7 @@ int mpcq_mimo_setup_plants_device(mpcq_ctx *c, int nx, int nu, int ny, int s_row
         }
     }
     if (flags & 2) return fail(MPCQ_ERR_SETUP, "mimo: a constraint row is not an inequality (|w0| beyond OSQP_INFTY)");
+    c->mimo_diag_k0 = (flags & 4) ? 0 : 1;
     c->last = s;
     c->fresh = true;  // the first step starts from x = z = y = 0, rho = settings.rho (initSolver, :64)
     c->mimo_ready = true;
@@ -1104,6 +1105,7 @@ int mpcq_mimo_step_device(mpcq_ctx *c, const double *X, double *U, const double 
     mpcq::MimoArgs a{};
     a.batch = c->dims.batch;
     a.N = c->mimo_N; a.nx = c->mimo_nx; a.nu = c->mimo_nu; a.ny = c->mimo_ny; a.s_rows = c->mimo_srows;
+    a.diag_k0 = c->mimo_diag_k0 && !std::getenv("MPCQ_MIMO_GENERAL_K0");  // (env: force the general path, tests)
     a.ops_stride = (size_t)mpcq::MimoLayout::make(a.N, a.nx, a.nu, a.ny).total;
     a.ops = c->d_mimo;
     a.st = to_solver(c->set);

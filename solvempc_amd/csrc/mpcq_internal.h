@@ -237,7 +237,8 @@ struct MimoSetupArgs {
     double sigma;
     const double *Ad, *Bd, *Cd, *Q, *R, *RD, *K, *K0, *w0;  // [plant] nx*nx, nx*nu, ny*nx, ny*ny, nu*nu x2, nu*nx, nu*nu, nu
     double *ops;                                            // [plant] MimoLayout::total
-    int *flags;                                             // OR: 1 setup failed, 2 a row is not an inequality
+    int *flags;                                             // OR: 1 setup failed, 2 a row is not an inequality,
+                                                            //     4 some K0 is not diagonal
     long long *stamps;                                      // debug (MPCQ_MIMO_SETUP_STAMPS): 16 per plant, or null
 };
 
@@ -252,6 +253,7 @@ struct MimoArgs {
     double *q_out, *u_out;      // batch*n, batch*2n: this step's q, u (unscaled)
     double *xs, *zs, *ys, *rhos;// scaled state (warm start): batch*n, batch*2n, batch*2n, batch
     int warm, fresh;
+    int diag_k0;                // every plant's K0 is diagonal: the A^ products need no cross-component mix
     double *x, *y;              // unscaled solution: batch*n, batch*2n
     int *status, *iter;
     double *rho_out;

@@ -181,6 +181,8 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
         P[(size_t)(j1 * nu + r) * ldp + j2 * nu + c] = s;
     }
     __syncthreads();
+    // Fu = 2 (R' + H(j, 0)) per block (:305, the .diagonal() quirk as blocks; Q symmetric): block j of
+    // sum_u CS_u' Q CS_(u+j) is G(j, N-1-j)', the last value of the scan over delta = j below
     for (int it = t; it < N * nu * nu; it += T) {
         const int dl = it / (nu * nu), r = (it / nu) % nu, c = it % nu;
         double acc = 0.0;
@@ -193,16 +195,9 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
             if (dl > 0)  // H(j2, j1) = H(j1, j2)'
                 P[(size_t)(j2 * nu + c) * ldp + j1 * nu + r] = 2.0 * (rr * R[c * nu + r] + acc);
         }
+        out[L.Fu + (dl * nu + c) * nu + r] = 2.0 * (R[r * nu + c] + acc);
     }
-    // Fu = 2 (R' + H(j, 0)) per block (:305, the .diagonal() quirk as blocks; Q symmetric),
     // Frs = -2 sum_{d <= N-1-j} QCS_d' (Fr = -2 (Qbar Su)', :306, summed over the horizon blocks)
-    for (int it = t; it < n * nu; it += T) {
-        const int j = it / (nu * nu), r = (it / nu) % nu, c = it % nu;
-        double acc = 0.0;
-        for (int i = j; i < N; i++)
-            acc += dot12(CS + (size_t)(i - j) * ny * nu + r, nu, QCS + (size_t)i * ny * nu + c, nu, ny);
-        out[L.Fu + it] = 2.0 * (R[c * nu + r] + acc);
-    }
     for (int it = t; it < n * ny; it += T) {
         const int j = it / (nu * ny), r = (it / ny) % nu, i = it % ny;
         double acc = 0.0;
@@ -229,7 +224,7 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
     // |A^((k, r), (j, c))| = E(k,r) |K0(r, c)| D(j, c) for j <= k, and the bottom rows mirror the top
     // ones (same norms, so the same E): column norms are suffix maxima over k, row norms prefix maxima.
     const int sc = t >> 7, cj = t & 127;  // column sweeps: column cj, row slice sc (8 x 16 rows)
-    auto colmax = [&]() {  // cm[0][j] = max_i D_i |P_ij| (needs a barrier before use)
+    auto colpart = [&]() {  // cm[sc][j] = max over the slice's rows of D_i |P_ij|
         if (cj < n) {
             double m0 = 0.0, m1 = 0.0;
             const int i0 = sc * 16;
@@ -241,13 +236,12 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
             }
             cm[sc * 128 + cj] = fmax(m0, m1);
         }
-        __syncthreads();
-        if (t < n) {
-            double m = cm[t];
+    };
+    auto colfull = [&](int j) {
+        double m = cm[j];
 #pragma unroll
-            for (int q = 1; q < 8; q++) m = fmax(m, cm[q * 128 + t]);
-            cm[t] = m;
-        }
+        for (int q = 1; q < 8; q++) m = fmax(m, cm[q * 128 + j]);
+        return m;
     };
     double cst = 1.0;
     for (int pass = 0; pass < a.scaling; pass++) {
@@ -262,8 +256,9 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
             wk[k * 4 + c] = w0;
             wk[128 + k * 4 + c] = w1;
         }
-        colmax();
+        colpart();
         __syncthreads();
+        double dt = 1.0, et = 1.0;
         if (t < n) {
             const int bj = t / nu, c = t % nu;
             double va = 0.0, vr = 0.0;
@@ -272,21 +267,21 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
                 if (k >= bj && k < N) va = fmax(va, wk[k * 4 + c]);
                 if (k <= bj) vr = fmax(vr, wk[128 + k * 4 + c]);
             }
-            const double v = fmax(cst * Dv[t] * cm[t], va * Dv[t]);
-            Dt[t] = 1.0 / sqrt(mimo_limit_scaling(v));
-            Et[t] = 1.0 / sqrt(mimo_limit_scaling(Ev[t] * vr));
+            const double v = fmax(cst * Dv[t] * colfull(t), va * Dv[t]);
+            dt = 1.0 / sqrt(mimo_limit_scaling(v));
+            et = 1.0 / sqrt(mimo_limit_scaling(Ev[t] * vr));
         }
-        __syncthreads();
+        __syncthreads();  // every column / row norm has read the old D, E
         if (t < n) {
-            Dv[t] *= Dt[t];
-            Ev[t] *= Et[t];
+            Dv[t] *= dt;
+            Ev[t] *= et;
         }
         __syncthreads();
-        colmax();  // norms of the rescaled P
+        colpart();  // norms of the rescaled P
         __syncthreads();
-        if (t < 64) {  // mean column norm (one wave), then the cost scaling
+        if (t < 64) {  // one wave: full column norms, their mean, the cost scaling
             double s = 0.0;
-            for (int j = t; j < n; j += 64) s += cst * Dv[j] * cm[j];
+            for (int j = t; j < n; j += 64) s += cst * Dv[j] * colfull(j);
             s = wsum(s);
             if (t == 0) {
                 const double mean = s / n;
@@ -310,6 +305,7 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
         // u0 = W0 (X = U = 0): a row with E w0 beyond OSQP_INFTY * MIN_SCALING would be free
         if (!(fabs(a.w0[(size_t)pl * nu + j % nu] * Ev[j]) < kInfty * kMinScaling)) atomicOr(a.flags, 2);
     }
+    if (t < nu * nu && t / nu != t % nu && K0[t] != 0.0) atomicOr(a.flags, 4);  // off-diagonal K0
     if (t == 0) {
         out[L.cs] = cst;
         out[L.cs + 1] = 1.0 / cst;
@@ -407,8 +403,11 @@ __device__ __forceinline__ double lane_suffix(double v, int lane)
         if (a.stamps && t == 0) a.stamps[(size_t)blockIdx.x * 8 + (k)] = (long long)(v);  \
     } while (0)
 
-template <int NU, int OCC>
-__global__ __launch_bounds__(kMimoThreads, OCC) void mimo_solve_kernel(MimoArgs a)
+#ifndef MPCQ_MIMO_WAVES_PER_EU
+#define MPCQ_MIMO_WAVES_PER_EU 2  // two QPs per CU (256 VGPRs); 3 spills the matrix path
+#endif
+template <int NU, bool DK>
+__global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_solve_kernel(MimoArgs a)
 {
     const int b = blockIdx.x;
     if (b >= a.batch) return;
@@ -431,7 +430,7 @@ __global__ __launch_bounds__(kMimoThreads, OCC) void mimo_solve_kernel(MimoArgs 
     __shared__ __attribute__((aligned(16))) double s_vec[kSegN];   // rhs (GEMV input)
     __shared__ __attribute__((aligned(16))) double s_nat[kSegN];   // warm start: x
     __shared__ __attribute__((aligned(16))) double s_out[kMimoN];  // GEMV output, component-major
-    __shared__ __attribute__((aligned(16))) double s_row[2][kSegN], s_col[2][kMimoN];
+    __shared__ __attribute__((aligned(16))) double s_row[2][kSegN];
     __shared__ double s_D[kMimoN], s_E[kMimoN], s_K0[16], s_SW[32 * 16];  // D, E component-major
     __shared__ double s_xb[4][kMimoN];  // scan exchange buffers (rotated: a buffer is rewritten 4 barriers later)
     __shared__ double s_red[2][4][16];  // cross-wave reductions (alternating)
@@ -537,26 +536,43 @@ __global__ __launch_bounds__(kMimoThreads, OCC) void mimo_solve_kernel(MimoArgs 
         for (int j = 0; j < NU; j++) acc = __builtin_fma(s_K0[j * 4 + (c & 3)], buf[j * 32 + (k & 31)], acc);
         return acc;
     };
-    // (A^ x)_top = E (L (x) K0) D x (the bottom half is its negation); x = this lane's element
+    // (A^ x)_top = E (L (x) K0) D x (the bottom half is its negation); x = this lane's element.  With
+    // every K0 diagonal (DK) the products are lane-local scans: no exchange, no barrier.
+    const double k0cc = s_K0[(c & 3) * 5];
     auto A_of = [&](double xv) {
-        const double *bf = scan_x(valid ? vD * xv : 0.0, false);
-        __syncthreads();
-        return valid ? vE * mix_plain(bf) : 0.0;
+        if constexpr (DK) {
+            const double p = lane_prefix(valid ? vD * xv : 0.0, lane);
+            return valid ? vE * (k0cc * p) : 0.0;
+        } else {
+            const double *bf = scan_x(valid ? vD * xv : 0.0, false);
+            __syncthreads();
+            return valid ? vE * mix_plain(bf) : 0.0;
+        }
     };
     // A^' [w_top; w_bot] = D (L (x) K0)' E d, d = w_top - w_bot
     auto At_of = [&](double d) {
-        const double *bf = scan_x(valid ? vE * d : 0.0, true);
-        __syncthreads();
-        return valid ? vD * mix_trans(bf) : 0.0;
+        if constexpr (DK) {
+            const double p = lane_suffix(valid ? vE * d : 0.0, lane);
+            return valid ? vD * (k0cc * p) : 0.0;
+        } else {
+            const double *bf = scan_x(valid ? vE * d : 0.0, true);
+            __syncthreads();
+            return valid ? vD * mix_trans(bf) : 0.0;
+        }
     };
     auto At_of2 = [&](double d1, double d2, double &o1, double &o2) {
         const double E = valid ? vE : 0.0;
-        const double *b1 = scan_x(E * d1, true);
-        const double *b2 = scan_x(E * d2, true);
-        __syncthreads();
-        const double D = vD;
-        o1 = valid ? D * mix_trans(b1) : 0.0;
-        o2 = valid ? D * mix_trans(b2) : 0.0;
+        if constexpr (DK) {
+            const double p1 = lane_suffix(E * d1, lane), p2 = lane_suffix(E * d2, lane);
+            o1 = valid ? vD * (k0cc * p1) : 0.0;
+            o2 = valid ? vD * (k0cc * p2) : 0.0;
+        } else {
+            const double *b1 = scan_x(E * d1, true);
+            const double *b2 = scan_x(E * d2, true);
+            __syncthreads();
+            o1 = valid ? vD * mix_trans(b1) : 0.0;
+            o2 = valid ? vD * mix_trans(b2) : 0.0;
+        }
     };
     // cross-wave max / sum of R per-lane values (uniform result in every thread)
     int rb = 0;
@@ -720,7 +736,6 @@ __global__ __launch_bounds__(kMimoThreads, OCC) void mimo_solve_kernel(MimoArgs 
     // of a step is barrier -> LDS reads -> 64 FMAs -> next writes: the next pivot's reciprocal is
     // computed one step ahead (its element is updated first, the division overlaps the FMAs) and
     // broadcast with the row, and the row owners scale their row in registers before the update.
-    __shared__ __attribute__((aligned(16))) double2 s_pv[2];  // (a_kk, 1 / a_kk)
     auto invert = [&]() {
         const int nkb = (n + 15) >> 4;
         double inv_next = 1.0 / Mb[0][0];  // meaningful on the owner of the next pivot only
@@ -731,16 +746,11 @@ __global__ __launch_bounds__(kMimoThreads, OCC) void mimo_solve_kernel(MimoArgs 
                 if (kp >= n) continue;  // (not break: the loop must fully unroll, or Mb leaves the VGPRs)
                 const int p = kp & 1;
                 const bool rown = rg == (kp >> 2), coln = cg == kb;
-                if (rown) {
+                if (rown) {  // row k, and (a_kk, 1 / a_kk) in the padding of the pivot's segment
                     double2 *r2 = (double2 *)&s_row[p][kSegLd * cg];
 #pragma unroll
                     for (int j = 0; j < 8; j++) r2[j] = make_double2(Mb[kk & 3][2 * j], Mb[kk & 3][2 * j + 1]);
-                    if (coln) s_pv[p] = make_double2(Mb[kk & 3][kk], inv_next);
-                }
-                if (coln) {
-                    double2 *c2 = (double2 *)&s_col[p][4 * rg];
-                    c2[0] = make_double2(Mb[0][kk], Mb[1][kk]);
-                    c2[1] = make_double2(Mb[2][kk], Mb[3][kk]);
+                    if (coln) r2[8] = make_double2(Mb[kk & 3][kk], inv_next);
                 }
                 __syncthreads();
 #ifdef MPCQ_GJ_STAMPS
@@ -749,17 +759,18 @@ __global__ __launch_bounds__(kMimoThreads, OCC) void mimo_solve_kernel(MimoArgs 
 #endif
                 const double2 *r2 = (const double2 *)&s_row[p][kSegLd * cg];
                 double2 q0 = r2[0], q1 = r2[1];  // row chunk 0, in flight with the column
-                const double2 pv = s_pv[p];
+                const double2 pv = *(const double2 *)&s_row[p][kSegLd * kb + 16];
                 if (!(pv.x > 0.0)) fail = 1;
                 const double inv = pv.y;
+                // column k from row k: the trailing block stays symmetric (a_ik = a_ki, i >= k) and the
+                // pivoted rows are its negation (a_ik = -a_ki, i < k: [A11^-1, A11^-1 A12; -A21 A11^-1, S])
                 double nci[4];  // -a_ik / a_kk (0 on row k itself: its owners scale it instead)
                 {
-                    const double2 *c2 = (const double2 *)&s_col[p][4 * rg];
+                    const double2 *c2 = (const double2 *)&s_row[p][kSegLd * (rg >> 2) + 4 * (rg & 3)];
                     const double2 u0 = c2[0], u1 = c2[1];
-                    nci[0] = -u0.x * inv;
-                    nci[1] = -u0.y * inv;
-                    nci[2] = -u1.x * inv;
-                    nci[3] = -u1.y * inv;
+                    const double cv[4] = {u0.x, u0.y, u1.x, u1.y};
+#pragma unroll
+                    for (int i = 0; i < 4; i++) nci[i] = (4 * rg + i < kp ? cv[i] : -cv[i]) * inv;
                 }
                 // lookahead: the next pivot's element first, its reciprocal overlapping the FMAs
                 {
@@ -1053,17 +1064,12 @@ extern "C" int mpcq_internal_mimo_solve_launch(const mpcq::MimoArgs *a, hipStrea
 {
     if (a->nx > 12 || a->ny > 12 || a->N * a->nu > mpcq::kMimoN || a->N > 32) return -1;
     const dim3 grid(a->batch), block(mpcq::kMimoThreads);
-    // waves per SIMD: 3 (168 VGPRs, three QPs per CU) or 2 (256 VGPRs, no spills); MPCQ_MIMO_OCC
-    static const int occ = [] {
-        const char *v = std::getenv("MPCQ_MIMO_OCC");
-        return (v && *v == '3') ? 3 : 2;
-    }();
 #define MPCQ_MIMO_LAUNCH(U)                                                                  \
     do {                                                                                     \
-        if (occ == 2)                                                                        \
-            hipLaunchKernelGGL((mpcq::mimo_solve_kernel<U, 2>), grid, block, 0, s, *a);      \
+        if (a->diag_k0)                                                                      \
+            hipLaunchKernelGGL((mpcq::mimo_solve_kernel<U, true>), grid, block, 0, s, *a);   \
         else                                                                                 \
-            hipLaunchKernelGGL((mpcq::mimo_solve_kernel<U, 3>), grid, block, 0, s, *a);      \
+            hipLaunchKernelGGL((mpcq::mimo_solve_kernel<U, false>), grid, block, 0, s, *a);  \
     } while (0)
     switch (a->nu) {
     case 1: MPCQ_MIMO_LAUNCH(1); break;

@@ -4,6 +4,6 @@
 set -e
 cd "$(dirname "$0")/../solvempc_amd/csrc"
 mkdir -p ../../tools/dbg
-/opt/rocm/bin/hipcc -O3 -ffp-contract=off -fno-slp-vectorize -std=c++17 -fPIC --offload-arch=gfx950 -D$1 -c mpcq_mimo.hip -o ../../tools/dbg/mpcq_mimo.o
+/opt/rocm/bin/hipcc -O3 -ffp-contract=off -fno-slp-vectorize -std=c++17 -fPIC --offload-arch=gfx950 $(for d in "$@"; do printf -- "-D%s " "$d"; done) -c mpcq_mimo.hip -o ../../tools/dbg/mpcq_mimo.o
 objs=$(ls build/*.o | grep -v mpcq_mimo)
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ../../tools/dbg/libmpcq.so $objs ../../tools/dbg/mpcq_mimo.o
