@@ -50,7 +50,8 @@ struct MimoSetupShape {
         s.N = N; s.nx = nx; s.nu = nu; s.ny = ny; s.n = N * nu;
         s.ldp = s.n + 1;  // odd stride: column walks by consecutive lanes hit distinct banks
         size_t o = 0;
-        s.P = o; o += (size_t)s.n * s.ldp > (size_t)N * ny * nx ? (size_t)s.n * s.ldp : (size_t)N * ny * nx;
+        const size_t hist = (size_t)N * (nx * nx + ny * nx + nx * nu);  // powers, QCA and Ad^d Bd histories
+        s.P = o; o += (size_t)s.n * s.ldp > hist ? (size_t)s.n * s.ldp : hist;
         s.Ad = o; o += (size_t)nx * nx;
         s.Bd = o; o += (size_t)nx * nu;
         s.Cd = o; o += (size_t)ny * nx;
@@ -103,7 +104,6 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
     double *RD = sm + S.RD, *K0 = sm + S.K0, *AB = sm + S.AB, *CA = sm + S.CA, *CS = sm + S.CS, *QCS = sm + S.QCS;
     double *Dv = sm + S.Dv, *Ev = sm + S.Ev, *Dt = sm + S.Dt, *Et = sm + S.Et, *cm = sm + S.cm, *wk = sm + S.wk;
     double *red = sm + S.red, *sh = sm + S.sh;
-    double *QCAh = P;  // QCA_d history, [d][ny][nx], until P is built
     const MimoLayout L = MimoLayout::make(N, nx, nu, ny);
     double *out = a.ops + (size_t)pl * L.total;
 #define MPCQ_SSTAMP(k)                                                                              \
@@ -129,30 +129,51 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
     MPCQ_SSTAMP(1);
 
     // ---- setTransformations (:187-204): CS_d = sum_{k<=d} Cd Ad^k Bd (the distinct blocks of Su) and
-    // QCA_d = Q Cd Ad^(d+1) (for Fx = 2 (Sx' Qbar Su)', :307); one barrier per horizon step, the four
-    // small products of a step on disjoint thread ranges
-    for (int e = t; e < ny * nx; e += T) CA[e] = dot12(Cd + (e / nx) * nx, 1, Ad + e % nx, nx, nx);  // Sx_0 = Cd Ad
+    // QCA_d = Q Cd Ad^(d+1) (for Fx = 2 (Sx' Qbar Su)', :307).  The powers Ad^k (k <= N) by doubling
+    // (log2 N barriers instead of one per horizon step), then every product of a horizon step at once.
+    double *Pw = P;                                     // Ad^k at Pw + (k-1) nx^2, k = 1..N
+    double *QCAh = P + (size_t)N * nx * nx;             // QCA_d, [d][ny][nx]
+    double *ABh = QCAh + (size_t)N * ny * nx;           // Ad^d Bd, [d][nx][nu]
+    double *QC = CA;                                    // Q Cd (ny x nx)
+    for (int e = t; e < nx * nx; e += T) Pw[e] = Ad[e];
+    for (int e = t; e < ny * nx; e += T) QC[e] = dot12(Q + (e / nx) * ny, 1, Cd + e % nx, nx, ny);
+    for (int e = t; e < nx * nu; e += T) ABh[e] = Bd[e];
     __syncthreads();
-    for (int d = 0; d < N; d++) {
-        const double *ABc = AB + (d & 1) * nx * nu, *CAc = CA + (d & 1) * ny * nx;
-        double *ABn = AB + ((d + 1) & 1) * nx * nu, *CAn = CA + ((d + 1) & 1) * ny * nx;
-        const int t1 = ny * nu, t2 = t1 + ny * nx, t3 = t2 + ny * nx, t4 = t3 + nx * nu;
-        if (t < t1) {
-            const int i = t / nu, c = t % nu;
-            const double cab = dot12(Cd + i * nx, 1, ABc + c, nu, nx);
-            CS[(size_t)d * ny * nu + t] = (d ? CS[(size_t)(d - 1) * ny * nu + t] : 0.0) + cab;
-        } else if (t < t2) {
-            const int e = t - t1, i = e / nx, c = e % nx;
-            QCAh[(size_t)d * ny * nx + e] = dot12(Q + i * ny, 1, CAc + c, nx, ny);
-        } else if (t < t3) {
-            const int e = t - t2, i = e / nx, c = e % nx;
-            CAn[e] = dot12(CAc + i * nx, 1, Ad + c, nx, nx);
-        } else if (t < t4) {
-            const int e = t - t3, i = e / nu, c = e % nu;
-            ABn[e] = dot12(Ad + i * nx, 1, ABc + c, nu, nx);
+    for (int have = 1; have < N; have *= 2) {  // Ad^k = Ad^have Ad^(k - have), have < k <= 2 have
+        const int fresh = (2 * have < N ? 2 * have : N) - have;
+        for (int it = t; it < fresh * nx * nx; it += T) {
+            const int kk = have + 1 + it / (nx * nx), i = (it / nx) % nx, j = it % nx;
+            Pw[(size_t)(kk - 1) * nx * nx + i * nx + j] =
+                dot12(Pw + (size_t)(have - 1) * nx * nx + i * nx, 1, Pw + (size_t)(kk - have - 1) * nx * nx + j, nx, nx);
         }
         __syncthreads();
     }
+    {
+        const int n1 = (N - 1) * nx * nu, n2 = N * ny * nx;
+        for (int it = t; it < n1 + n2; it += T) {
+            if (it < n1) {  // Ad^d Bd, d >= 1
+                const int d = 1 + it / (nx * nu), i = (it / nu) % nx, c = it % nu;
+                ABh[(size_t)d * nx * nu + i * nu + c] = dot12(Pw + (size_t)(d - 1) * nx * nx + i * nx, 1, Bd + c, nu, nx);
+            } else {  // QCA_d = (Q Cd) Ad^(d+1)
+                const int e = it - n1, d = e / (ny * nx), i = (e / nx) % ny, c = e % nx;
+                QCAh[e] = dot12(QC + i * nx, 1, Pw + (size_t)d * nx * nx + c, nx, nx);
+            }
+        }
+    }
+    __syncthreads();
+    for (int it = t; it < N * ny * nu; it += T) {  // Cd Ad^d Bd
+        const int d = it / (ny * nu), i = (it / nu) % ny, c = it % nu;
+        CS[it] = dot12(Cd + i * nx, 1, ABh + (size_t)d * nx * nu + c, nu, nx);
+    }
+    __syncthreads();
+    for (int e = t; e < ny * nu; e += T) {  // prefix over the horizon
+        double acc = 0.0;
+        for (int d = 0; d < N; d++) {
+            acc += CS[(size_t)d * ny * nu + e];
+            CS[(size_t)d * ny * nu + e] = acc;
+        }
+    }
+    __syncthreads();
     MPCQ_SSTAMP(2);
     // Fx_j = 2 sum_{d >= j} CS_{d-j}' QCA_d  (block row j, nu x nx); QCS_d = Q CS_d
     for (int it = t; it < n * nx; it += T) {
@@ -224,7 +245,7 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
     // |A^((k, r), (j, c))| = E(k,r) |K0(r, c)| D(j, c) for j <= k, and the bottom rows mirror the top
     // ones (same norms, so the same E): column norms are suffix maxima over k, row norms prefix maxima.
     const int sc = t >> 7, cj = t & 127;  // column sweeps: column cj, row slice sc (8 x 16 rows)
-    auto colpart = [&]() {  // cm[sc][j] = max over the slice's rows of D_i |P_ij|
+    auto colpart = [&](const double *Dv) {  // cm[sc][j] = max over the slice's rows of D_i |P_ij|
         if (cj < n) {
             double m0 = 0.0, m1 = 0.0;
             const int i0 = sc * 16;
@@ -243,22 +264,37 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
         for (int q = 1; q < 8; q++) m = fmax(m, cm[q * 128 + j]);
         return m;
     };
+    // One column sweep per pass: pass p's Dt uses the norms of c_p D_p P D_p, and pass p-1's cost
+    // scaling uses the norms of c_(p-1) D_p P D_p -- the same sweep.  Per pass: sweep | column norms,
+    // A-norm block maxima, mean partials | cost scaling of the previous pass, Dt, Et, D, E | ...
     double cst = 1.0;
-    for (int pass = 0; pass < a.scaling; pass++) {
-        // A-norm block maxima: wk[0][k][c] = max_r E(k,r) |K0(r,c)|, wk[1][k][r] = max_c |K0(r,c)| D(k,c)
+    double *Dc = Dv, *Dn = Dt, *Ec = Ev, *En = Et;  // current / next scaling (double-buffered)
+    colpart(Dc);
+    for (int pass = 0; pass <= a.scaling; pass++) {
+        __syncthreads();  // the sweep's partials; the previous pass's D, E
+        double cmt = 0.0;
         if (t < n) {
+            cmt = colfull(t);
             const int k = t / nu, c = t % nu;
-            double w0 = 0.0, w1 = 0.0;
+            double w0 = 0.0, w1 = 0.0;  // A-norm block maxima: max_r E(k,r) |K0(r,c)|, max_q |K0(c,q)| D(k,q)
             for (int q = 0; q < nu; q++) {
-                w0 = fmax(w0, Ev[k * nu + q] * fabs(K0[q * nu + c]));
-                w1 = fmax(w1, fabs(K0[c * nu + q]) * Dv[k * nu + q]);
+                w0 = fmax(w0, Ec[k * nu + q] * fabs(K0[q * nu + c]));
+                w1 = fmax(w1, fabs(K0[c * nu + q]) * Dc[k * nu + q]);
             }
             wk[k * 4 + c] = w0;
             wk[128 + k * 4 + c] = w1;
         }
-        colpart();
+        if (pass > 0 && t < 128) {  // mean column norm of c D P D (previous pass's cost scaling)
+            const double sv = wsum(t < n ? cst * Dc[t] * cmt : 0.0);
+            if ((t & 63) == 0) red[t >> 6] = sv;
+        }
         __syncthreads();
-        double dt = 1.0, et = 1.0;
+        if (pass > 0) {
+            const double mean = (red[0] + red[1]) / n;
+            const double qn = mimo_limit_scaling(0.0);  // |q^| = 0 at setup
+            cst *= 1.0 / mimo_limit_scaling(fmax(mean, qn));
+        }
+        if (pass == a.scaling) break;
         if (t < n) {
             const int bj = t / nu, c = t % nu;
             double va = 0.0, vr = 0.0;
@@ -267,30 +303,21 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
                 if (k >= bj && k < N) va = fmax(va, wk[k * 4 + c]);
                 if (k <= bj) vr = fmax(vr, wk[128 + k * 4 + c]);
             }
-            const double v = fmax(cst * Dv[t] * colfull(t), va * Dv[t]);
-            dt = 1.0 / sqrt(mimo_limit_scaling(v));
-            et = 1.0 / sqrt(mimo_limit_scaling(Ev[t] * vr));
+            const double v = fmax(cst * Dc[t] * cmt, va * Dc[t]);
+            Dn[t] = Dc[t] / sqrt(mimo_limit_scaling(v));
+            En[t] = Ec[t] / sqrt(mimo_limit_scaling(Ec[t] * vr));
         }
-        __syncthreads();  // every column / row norm has read the old D, E
+        __syncthreads();
+        double *tp = Dc; Dc = Dn; Dn = tp;
+        tp = Ec; Ec = En; En = tp;
+        colpart(Dc);  // norms of the rescaled P
+    }
+    if (Dc != Dv) {  // the final scaling back in Dv, Ev
         if (t < n) {
-            Dv[t] *= dt;
-            Ev[t] *= et;
+            Dv[t] = Dc[t];
+            Ev[t] = Ec[t];
         }
         __syncthreads();
-        colpart();  // norms of the rescaled P
-        __syncthreads();
-        if (t < 64) {  // one wave: full column norms, their mean, the cost scaling
-            double s = 0.0;
-            for (int j = t; j < n; j += 64) s += cst * Dv[j] * colfull(j);
-            s = wsum(s);
-            if (t == 0) {
-                const double mean = s / n;
-                const double qn = mimo_limit_scaling(0.0);  // |q^| = 0 at setup
-                sh[1] = 1.0 / mimo_limit_scaling(fmax(mean, qn));
-            }
-        }
-        __syncthreads();
-        cst *= sh[1];
     }
     MPCQ_SSTAMP(6);
 
