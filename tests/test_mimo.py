@@ -125,3 +125,31 @@ def test_second_step_is_warm_started():
                 u_cur = u_cur + r.x()[:4]
             np.testing.assert_allclose(Us[k][b], u_cur, rtol=0, atol=1e-7)
         assert st[b] == r.info().status
+
+
+@pytest.mark.parametrize("over", [dict(max_iter=15), dict(adaptive_rho=0), dict(check_termination=5),
+                                  dict(eps_abs=1e-5, eps_rel=1e-5), dict(scaling=0), dict(alpha=1.0, rho=1.0)],
+                         ids=["max_iter", "no_adapt", "check5", "tight", "unscaled", "alpha1_rho1"])
+def test_settings_variants_match_oracle(over):
+    """OSQP settings the reference could set (osqp-eigen settings(), :51-52) on the quad-rotor batch:
+    statuses (MAX_ITER_REACHED / SOLVED_INACCURATE included), iteration schedule and solutions."""
+    N, B = 30, 16
+    Ad, Bd = workload.quadrotor_plants(7, 0, B)
+    sh = workload.quadrotor_shared()
+    X, U = workload.quadrotor_states(7, 0, B)
+    Us, x, st, it = _run_device(sh, Ad, Bd, X, U, N, settings=sm.default_settings(**over))
+    U_ref, x_ref, st_ref, it_ref = oracle.mimo_plants_step(sh, Ad, Bd, X, U, N, settings=oracle.default_settings(**over),
+                                                           nthreads=8)
+    _check(x, st, it, Us[0], x_ref, st_ref, it_ref, U_ref)
+
+
+def test_general_k0_path_on_diagonal_k0(monkeypatch):
+    """The exchange path (general K0) run on the quad-rotor (diagonal K0) gives the oracle's results too."""
+    monkeypatch.setenv("MPCQ_MIMO_GENERAL_K0", "1")
+    N, B = 30, 12
+    Ad, Bd = workload.quadrotor_plants(9, 0, B)
+    sh = workload.quadrotor_shared()
+    X, U = workload.quadrotor_states(9, 0, B)
+    Us, x, st, it = _run_device(sh, Ad, Bd, X, U, N)
+    U_ref, x_ref, st_ref, it_ref = oracle.mimo_plants_step(sh, Ad, Bd, X, U, N, nthreads=8)
+    _check(x, st, it, Us[0], x_ref, st_ref, it_ref, U_ref)
