@@ -645,7 +645,7 @@ static int launch_args(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s)
             a.stop_iter = c->set.max_iter;
             rc = wave_launch<T>(c, a, p == 0 ? B : std::min(B, 2048), s);
             if (rc) return rc;
-            np_run = p;
+            np_run = p + (stp && *stp ? 1 : 0);  // (the stamps dump includes the wave launch)
             break;
         } else
             rc = std::is_same<T, float>::value

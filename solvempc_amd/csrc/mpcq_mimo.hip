@@ -43,15 +43,17 @@ __device__ inline double mimo_limit_scaling(double d)
 // big region; before P is built it holds the history QCA_d = Q Cd Ad^(d+1) of the recurrences.
 struct MimoSetupShape {
     int N, nx, nu, ny, n, ldp;
-    size_t P, Ad, Bd, Cd, Q, R, RD, K0, AB, CA, CS, QCS, Dv, Ev, Dt, Et, cm, wk, red, sh, total;
+    size_t hist, P, Ad, Bd, Cd, Q, R, RD, K0, AB, CA, CS, QCS, Dv, Ev, Dt, Et, cm, wk, red, sh, total;
     __host__ __device__ static MimoSetupShape make(int N, int nx, int nu, int ny)
     {
         MimoSetupShape s{};
         s.N = N; s.nx = nx; s.nu = nu; s.ny = ny; s.n = N * nu;
         s.ldp = s.n + 1;  // odd stride: column walks by consecutive lanes hit distinct banks
         size_t o = 0;
-        const size_t hist = (size_t)N * (nx * nx + ny * nx + nx * nu);  // powers, QCA and Ad^d Bd histories
-        s.P = o; o += (size_t)s.n * s.ldp > hist ? (size_t)s.n * s.ldp : hist;
+        // powers, QCA and Ad^d Bd histories, then the Fx partial tiles ((n+15)/16 x 256)
+        s.hist = (size_t)N * (nx * nx + ny * nx + nx * nu);
+        const size_t scratch = s.hist + (size_t)((s.n + 15) / 16) * 256;
+        s.P = o; o += (size_t)s.n * s.ldp > scratch ? (size_t)s.n * s.ldp : scratch;
         s.Ad = o; o += (size_t)nx * nx;
         s.Bd = o; o += (size_t)nx * nu;
         s.Cd = o; o += (size_t)ny * nx;
@@ -175,13 +177,39 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
     }
     __syncthreads();
     MPCQ_SSTAMP(2);
-    // Fx_j = 2 sum_{d >= j} CS_{d-j}' QCA_d  (block row j, nu x nx); QCS_d = Q CS_d
-    for (int it = t; it < n * nx; it += T) {
-        const int j = it / (nu * nx), r = (it / nx) % nu, c = it % nx;
-        double acc = 0.0;
-        for (int d = j; d < N; d++)
-            acc += dot12(CS + (size_t)(d - j) * ny * nu + r, nu, QCAh + (size_t)d * ny * nx + c, nx, ny);
-        out[L.Fx + it] = 2.0 * acc;
+    // Fx_j = 2 sum_{d >= j} CS_{d-j}' QCA_d (block row j, nu x nx) on the matrix cores: Fx = sum_d A_d B_d
+    // with A_d((j,r), kk) = CS_{d-j}(kk, r) (j <= d) and B_d = QCA_d, every horizon step accumulated in
+    // the same 16 x 16 output tile (rows (j, r), columns c < nx <= 16); two waves per row tile split the
+    // steps by parity and add through LDS.  QCS_d = Q CS_d.
+    {
+        typedef double v4d __attribute__((ext_vector_type(4)));
+        const int lane = t & 63, wv = t >> 6, nt = (n + 15) >> 4, nks = (ny + 3) >> 2;
+        double *part = P + S.hist;  // [tile][64 lanes][4], past the live histories
+        const int ti = wv % 8, half = wv / 8;
+        v4d acc = {0.0, 0.0, 0.0, 0.0};
+        if (ti < nt) {
+            const int g = ti * 16 + (lane & 15), j = g / nu, r = g % nu, cc = lane & 15;
+            for (int d = half; d < N; d += 2) {
+                for (int ks = 0; ks < nks; ks++) {
+                    const int kk = ks * 4 + (lane >> 4);
+                    const double av = (g < n && kk < ny && j <= d) ? CS[((size_t)(d - j) * ny + kk) * nu + r] : 0.0;
+                    const double bv = (cc < nx && kk < ny) ? QCAh[((size_t)d * ny + kk) * nx + cc] : 0.0;
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+                }
+            }
+            if (half == 1)
+#pragma unroll
+                for (int v = 0; v < 4; v++) part[((size_t)ti * 64 + lane) * 4 + v] = acc[v];
+        }
+        __syncthreads();
+        if (ti < nt && half == 0) {
+#pragma unroll
+            for (int v = 0; v < 4; v++) {  // D(row = (lane >> 4) + 4 v, col = lane & 15)
+                const int g = ti * 16 + (lane >> 4) + 4 * v, c = lane & 15;
+                const double f = acc[v] + part[((size_t)ti * 64 + lane) * 4 + v];
+                if (g < n && c < nx) out[L.Fx + (size_t)g * nx + c] = 2.0 * f;
+            }
+        }
     }
     for (int e = t; e < N * ny * nu; e += T) {
         const int d = e / (ny * nu), i = (e / nu) % ny, c = e % nu;
@@ -192,14 +220,36 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
 
     // ---- setH (:250-251): H(j1, j1+delta) = G(delta, N-1-j1-delta), G(delta, T) = sum_{t<=T}
     // CS_{t+delta}' Q CS_t; H1 = 2 ((N - max(j1, j2)) R + RD delta_{j1 j2} + H) (LL' Rbar LL has block
-    // (j1, j2) = sum_{k >= max} R); P = (H1 + H1') / 2.  The N^2 nu^2 block products in parallel into
-    // their P slots, then one prefix scan over T per (delta, r, c).
-    for (int it = t; it < N * N * nu * nu; it += T) {
-        const int dl = it / (N * nu * nu), tt = (it / (nu * nu)) % N, r = (it / nu) % nu, c = it % nu;
-        if (tt + dl >= N) continue;
-        const double s = dot12(CS + (size_t)(tt + dl) * ny * nu + r, nu, QCS + (size_t)tt * ny * nu + c, nu, ny);
-        const int j2 = N - 1 - tt, j1 = j2 - dl;
-        P[(size_t)(j1 * nu + r) * ldp + j2 * nu + c] = s;
+    // (j1, j2) = sum_{k >= max} R); P = (H1 + H1') / 2.  The block products are one GEMM on the matrix
+    // cores, Z = CS' (Q CS) with CS = [CS_0 .. CS_{N-1}] (n_y x n): Z((i,r),(k,c)) = (CS_i' Q CS_k)(r,c),
+    // needed for i >= k (delta = i - k, T = k) -- v_mfma_f64_16x16x4_f64 over the lower 16 x 16 tiles,
+    // each product stored to its P slot (row block N-1-i, column block N-1-k); then one prefix scan over
+    // T per (delta, r, c).
+    {
+        typedef double v4d __attribute__((ext_vector_type(4)));
+        const int lane = t & 63, wv = t >> 6, nt = (n + 15) >> 4, nks = (ny + 3) >> 2;
+        const int ntiles = nt * (nt + 1) / 2;
+        for (int tile = wv; tile < ntiles; tile += T / 64) {  // wave-uniform: (ti >= tk) pairs
+            int ti = 0, rem = tile;
+            while (rem > ti) { rem -= ti + 1; ti++; }
+            const int tk = rem;
+            const int ga = ti * 16 + (lane & 15), gb = tk * 16 + (lane & 15);  // A row / B column of this lane
+            const int ia = ga / nu, ra = ga % nu, kb = gb / nu, cb = gb % nu;
+            v4d acc = {0.0, 0.0, 0.0, 0.0};
+            for (int ks = 0; ks < nks; ks++) {
+                const int kk = ks * 4 + (lane >> 4);
+                const double av = (ga < n && kk < ny) ? CS[((size_t)ia * ny + kk) * nu + ra] : 0.0;
+                const double bv = (gb < n && kk < ny) ? QCS[((size_t)kb * ny + kk) * nu + cb] : 0.0;
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int v = 0; v < 4; v++) {  // D(row = (lane >> 4) + 4 v, col = lane & 15)
+                const int gi = ti * 16 + (lane >> 4) + 4 * v, gk = gb;
+                const int i = gi / nu, r = gi % nu, k = kb, c = cb;
+                if (gi < n && gk < n && i >= k)
+                    P[(size_t)((N - 1 - i) * nu + r) * ldp + (N - 1 - k) * nu + c] = acc[v];
+            }
+        }
     }
     __syncthreads();
     // Fu = 2 (R' + H(j, 0)) per block (:305, the .diagonal() quirk as blocks; Q symmetric): block j of

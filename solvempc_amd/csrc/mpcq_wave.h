@@ -245,8 +245,17 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
     int next_adapt = ai ? (it / ai + 1) * ai : -1;
     const T *Einv_p = ops + L.Einv;
     const T *Dinv_p = ops + L.Dinv;
+#ifdef MPCQ_WAVE_STAMPS
+#define MPCQ_WSTAMP(k)                                                                                  \
+    do {                                                                                                \
+        if (a.stamps && blockIdx.x < 2048 && (it == 140 || it == 141)) a.stamps[(size_t)blockIdx.x * 16 + (it - 140) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define MPCQ_WSTAMP(k) do { } while (0)
+#endif
     for (;;) {
         it++;
+        MPCQ_WSTAMP(0);
         const bool at_check = it == next_check;
         const bool at_adapt = it == next_adapt;
         if (at_check) next_check += ct;
@@ -265,6 +274,7 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
         if (ln) bcx[lane] = xs;
         if (lm) bcw[lane] = w;
         __syncthreads();
+        MPCQ_WSTAMP(1);
         T xi = row_dot(Srow, bcx, gk) + row_dot(Btrow, bcw, T(0));  // two independent chains
         const T eta = xi * dk;
         const T xn = ln ? tt_fma(alpha, eta, oma * xs) : T(0);
@@ -272,8 +282,10 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
         xs = xn;
         // ---- z~ = B eta ; relaxation ; projection ; dual update
         __syncthreads();
+        MPCQ_WSTAMP(2);
         if (ln) bcx[lane] = eta;
         __syncthreads();
+        MPCQ_WSTAMP(3);
         const T zt = row_dot(Brow, bcx, T(0));
         T dy = T(0);
         if (lm) {
@@ -285,6 +297,7 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
             y = tt_fma(rj, v - zn, y);
             z = zn;
         }
+        MPCQ_WSTAMP(4);
         if (!info) continue;
 
         // ---- update_info: residual norms (whole-wave reductions)
