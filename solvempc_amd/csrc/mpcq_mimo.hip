@@ -38,6 +38,41 @@ __device__ inline double mimo_limit_scaling(double d)
     return d > kMaxScaling ? kMaxScaling : d;
 }
 
+// inclusive max scans over lanes 0..31 of non-negative values (DPP row shifts read 0 outside the row,
+// then one cross-row readlane); lanes >= 32 are ignored by the callers
+template <int CTRL> __device__ __forceinline__ double dpp_zero(double v)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xF, 0xF, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ double readlane_f64(double v, int l)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ double lane_prefix_max(double v, int lane)
+{
+    v = fmax(v, dpp_zero<0x111>(v));
+    v = fmax(v, dpp_zero<0x112>(v));
+    v = fmax(v, dpp_zero<0x114>(v));
+    v = fmax(v, dpp_zero<0x118>(v));
+    const double s = readlane_f64(v, 15);
+    return (lane >= 16) ? fmax(v, s) : v;
+}
+__device__ __forceinline__ double lane_suffix_max(double v, int lane)
+{
+    v = fmax(v, dpp_zero<0x101>(v));
+    v = fmax(v, dpp_zero<0x102>(v));
+    v = fmax(v, dpp_zero<0x104>(v));
+    v = fmax(v, dpp_zero<0x108>(v));
+    const double s = readlane_f64(v, 16);
+    return (lane < 16) ? fmax(v, s) : v;
+}
+
 // ----------------------------------------------------------------------------------------------
 // setup: one 1024-thread workgroup (16 waves) per plant; LDS carve (doubles).  P (n x (n+1)) is the
 // big region; before P is built it holds the history QCA_d = Q Cd Ad^(d+1) of the recurrences.
@@ -321,18 +356,29 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
     double *Dc = Dv, *Dn = Dt, *Ec = Ev, *En = Et;  // current / next scaling (double-buffered)
     colpart(Dc);
     for (int pass = 0; pass <= a.scaling; pass++) {
+        if (pass == 1) MPCQ_SSTAMP(8);
         __syncthreads();  // the sweep's partials; the previous pass's D, E
+        if (pass == 1) MPCQ_SSTAMP(9);
         double cmt = 0.0;
-        if (t < n) {
-            cmt = colfull(t);
-            const int k = t / nu, c = t % nu;
-            double w0 = 0.0, w1 = 0.0;  // A-norm block maxima: max_r E(k,r) |K0(r,c)|, max_q |K0(c,q)| D(k,q)
-            for (int q = 0; q < nu; q++) {
-                w0 = fmax(w0, Ec[k * nu + q] * fabs(K0[q * nu + c]));
-                w1 = fmax(w1, fabs(K0[c * nu + q]) * Dc[k * nu + q]);
+        if (t < n) cmt = colfull(t);
+        if ((t >> 6) == 2) {  // wave 2 (no column of its own), lane k = block k: A-norm block maxima and
+                              // their suffix / prefix maxima
+            const int k = t & 63;
+#pragma unroll
+            for (int c = 0; c < 4; c++) {  // (all four scans in flight; components >= nu are zero)
+                double w0 = 0.0, w1 = 0.0;  // max_r E(k,r) |K0(r,c)|, max_q |K0(c,q)| D(k,q)
+                if (k < N && c < nu)
+                    for (int q = 0; q < nu; q++) {
+                        w0 = fmax(w0, Ec[k * nu + q] * fabs(K0[q * nu + c]));
+                        w1 = fmax(w1, fabs(K0[c * nu + q]) * Dc[k * nu + q]);
+                    }
+                w0 = lane_suffix_max(w0, k);
+                w1 = lane_prefix_max(w1, k);
+                if (k < 32) {
+                    wk[k * 4 + c] = w0;
+                    wk[128 + k * 4 + c] = w1;
+                }
             }
-            wk[k * 4 + c] = w0;
-            wk[128 + k * 4 + c] = w1;
         }
         if (pass > 0 && t < 128) {  // mean column norm of c D P D (previous pass's cost scaling)
             const double sv = wsum(t < n ? cst * Dc[t] * cmt : 0.0);
@@ -345,19 +391,16 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
             cst *= 1.0 / mimo_limit_scaling(fmax(mean, qn));
         }
         if (pass == a.scaling) break;
+        if (pass == 1) MPCQ_SSTAMP(10);
         if (t < n) {
             const int bj = t / nu, c = t % nu;
-            double va = 0.0, vr = 0.0;
-#pragma unroll
-            for (int k = 0; k < 32; k++) {  // suffix / prefix maxima over blocks (32 independent loads)
-                if (k >= bj && k < N) va = fmax(va, wk[k * 4 + c]);
-                if (k <= bj) vr = fmax(vr, wk[128 + k * 4 + c]);
-            }
+            const double va = wk[bj * 4 + c], vr = wk[128 + bj * 4 + c];  // suffix / prefix maxima (wave 0)
             const double v = fmax(cst * Dc[t] * cmt, va * Dc[t]);
             Dn[t] = Dc[t] / sqrt(mimo_limit_scaling(v));
             En[t] = Ec[t] / sqrt(mimo_limit_scaling(Ec[t] * vr));
         }
         __syncthreads();
+        if (pass == 1) MPCQ_SSTAMP(11);
         double *tp = Dc; Dc = Dn; Dn = tp;
         tp = Ec; Ec = En; En = tp;
         colpart(Dc);  // norms of the rescaled P
