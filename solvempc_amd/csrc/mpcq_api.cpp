@@ -35,6 +35,8 @@ int fail(int code, const std::string &msg)
     } while (0)
 
 constexpr int kMaxPhases = 16;
+constexpr int kMaxSplit = 8;      // tile sub-batch chains (streams) per solve
+constexpr int kDefaultSplit = 1;  // measured: 4 parts on 4 streams ran no faster (0.52 vs 0.47 ms per cfg2 solve)
 
 size_t setup_scratch_len(int n, int m)
 {
@@ -54,6 +56,11 @@ struct mpcq_ctx {
     int KN = 0, KM = 0;
     void *d_img = nullptr;
     int *d_list = nullptr, *d_counts = nullptr, *d_itstate = nullptr;
+    unsigned *d_sched = nullptr;  // tile work queue: TileSched counters
+    int *d_qlist = nullptr;       //                  [stage][batch] queue entries
+    bool wq_last = false;         // the last solve ran the work queue (its error word is valid)
+    hipStream_t side[kMaxSplit] = {};     // tile sub-batch streams (side[0] unused: part 0 runs on the caller's)
+    hipEvent_t ev_split[kMaxSplit] = {};  // fork (0) / join (j) events of the sub-batch chains
     long long *d_stamps = nullptr;  // debug (MPCQ_TILE_STAMPS)
     hipStream_t last = nullptr;
     int nx = 0;
@@ -341,8 +348,10 @@ int mpcq_create(const mpcq_dims *d, const mpcq_settings *s, mpcq_ctx **out)
         const mpcq::TileLayout TL = mpcq::TileLayout::make(KN, KM, (int)(16 / es));
         A(&c->d_img, es * TL.total);
         A((void **)&c->d_list, 4 * 2 * B);
-        A((void **)&c->d_counts, 4 * kMaxPhases);
+        A((void **)&c->d_counts, 4 * kMaxPhases * kMaxSplit);
         A((void **)&c->d_itstate, 4 * B);
+        A((void **)&c->d_sched, 4 * mpcq::TileSched::kWords);
+        A((void **)&c->d_qlist, 4 * (size_t)mpcq::kMaxStages * B);
     } else if (!c->mimo_only) {
         A(&c->d_snx, es * B * nc);
         A(&c->d_sny, es * B * mc);
@@ -365,8 +374,12 @@ int mpcq_destroy(mpcq_ctx *c)
                     c->d_setup_status, c->d_q, c->d_u, c->d_l, c->d_x, c->d_y, c->d_rho, c->d_status, c->d_iter,
                     c->d_xs, c->d_zs, c->d_ys, c->d_rhos, c->d_snx, c->d_sny, c->d_Fx, c->d_Fu, c->d_Fr,
                     c->d_Sbar, c->d_Ku, c->d_W0, c->d_X, c->d_U, c->d_img, c->d_list, c->d_counts,
-                    c->d_itstate, c->d_Ad, c->d_Bd, c->d_step, c->d_flags, c->d_stamps, c->d_mimo};
+                    c->d_itstate, c->d_Ad, c->d_Bd, c->d_step, c->d_flags, c->d_stamps, c->d_mimo, c->d_sched, c->d_qlist};
     if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
+    for (int j = 0; j < kMaxSplit; j++) {
+        if (c->side[j]) (void)hipStreamDestroy(c->side[j]);
+        if (c->ev_split[j]) (void)hipEventDestroy(c->ev_split[j]);
+    }
     if (c->graph) (void)hipGraphDestroy(c->graph);
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
@@ -552,18 +565,19 @@ int mpcq_warm_start(mpcq_ctx *c, const double *x, const double *y)
 
 // Phase boundaries of the tile path (multiples of check_termination, then max_iter): QPs still
 // running at a boundary are re-packed densely into the waves of the next launch.
-static int phase_stops(const mpcq_settings &st, int *stops)
+static int phase_stops(const mpcq_settings &st, int *stops, bool queue = false)
 {
     const int ct = st.check_termination;
     int np = 0;
     const char *e = std::getenv("MPCQ_PHASES");  // test/benchmark hook: "0" = one launch per solve,
                                                   // or a comma list of check multiples ("3,4,5,6,8")
     int mult[kMaxPhases] = {3, 4, 5, 6, 8, 12, 20, 40, 80, 160};
-    int nm = 10;
+    int nm = queue ? 3 : 10;  // work queue: the few QPs past 5 checks finish in place (no more hand-offs)
+    const int cap = queue ? mpcq::kMaxStages : kMaxPhases;
     if (e && e[0] == '0') nm = 0;
     else if (e && *e) {
         nm = 0;
-        for (const char *p = e; *p && nm < kMaxPhases - 1;) {
+        for (const char *p = e; *p && nm < cap - 1;) {
             mult[nm++] = std::atoi(p);
             while (*p && *p != ',') p++;
             if (*p == ',') p++;
@@ -572,7 +586,7 @@ static int phase_stops(const mpcq_settings &st, int *stops)
     if (ct > 0) {
         for (int i = 0; i < nm; i++) {
             const long it = (long)mult[i] * ct;
-            if (it >= st.max_iter || np >= kMaxPhases - 1) break;
+            if (it >= st.max_iter || np >= cap - 1) break;
             if (np && it <= stops[np - 1]) continue;
             stops[np++] = (int)it;
         }
@@ -595,46 +609,37 @@ static int wave_launch(mpcq_ctx *c, const mpcq::AdmmArgs<T> &a, int grid, hipStr
                : mpcq_internal_wave_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->nc, c->mc, grid, s);
 }
 
+// The phase chain of QPs [lo, hi) of a tile context on stream s (part `part` of the batch: its own
+// two alternating QP lists in d_list[2 lo, 2 hi) and its own phase counters).
 template <typename T>
-static int launch_args(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s)
+static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, int lo, int hi, int part, bool wave_only)
 {
-    const int B = c->dims.batch;
-    if (!c->tile) {
-        // per-plant batches: one QP per wave (operators in VGPRs); the lane kernel for shapes the wave
-        // kernel does not compile (n > 32 or m > 64) or when forced by the test hook
-        if (std::strcmp(env_kernel(), "lane") != 0 && c->dims.n <= 32 && c->dims.m <= 64) {
-            a.stop_iter = c->set.max_iter;
-            return wave_launch<T>(c, a, B, s);
-        }
-        return std::is_same<T, float>::value
-                   ? mpcq_internal_admm_launch_f32((const mpcq::AdmmArgs<float> *)&a, c->nc, c->mc, s)
-                   : mpcq_internal_admm_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->nc, c->mc, s);
-    }
+    const int Bp = hi - lo;
     int stops[kMaxPhases];
     const int np = phase_stops(c->set, stops);
-    if (hipMemsetAsync(c->d_counts, 0, 4 * kMaxPhases, s) != hipSuccess) return -2;
+    int *const counts = c->d_counts + (size_t)part * kMaxPhases;
+    if (hipMemsetAsync(counts, 0, 4 * kMaxPhases, s) != hipSuccess) return -2;
     const int mpc = a.mpc;
-    // phases whose QPs are few (the slow tail) run one QP per wave
     const char *te = std::getenv("MPCQ_TAIL_PHASE");
-    const bool all_wave = std::strcmp(env_kernel(), "wave") == 0;
-    // Small batches (under 512 tile waves) are latency-bound: one QP per wave from the start.
-    const bool small = B < 8192 && std::strcmp(env_kernel(), "tile") != 0;
-    const int tail_from = (all_wave || small) ? 0 : (te ? std::atoi(te) : 3);
+    const int tail_from = wave_only ? 0 : (te ? std::atoi(te) : 3);
     int np_run = 0;
+    a.batch = Bp;
+    a.qp0 = lo;
 
-    // debug hook: per-wave stage stamps of every phase launch, written to $MPCQ_TILE_STAMPS after the solve
-    const char *stp = std::getenv("MPCQ_TILE_STAMPS");
-    const size_t waves = (size_t)(B + 15) / 16 + 4;
+    // debug hook (one part only): per-wave stage stamps of every phase launch, written to
+    // $MPCQ_TILE_STAMPS after the solve
+    const char *stp = part == 0 ? std::getenv("MPCQ_TILE_STAMPS") : nullptr;
+    const size_t waves = (size_t)(Bp + 15) / 16 + 4;
     if (stp && *stp && !c->d_stamps && hipMalloc((void **)&c->d_stamps, 8 * 8 * waves * kMaxPhases) != hipSuccess)
         return -2;
     if (stp && *stp && hipMemsetAsync(c->d_stamps, 0, 8 * 8 * waves * kMaxPhases, s) != hipSuccess) return -2;
     for (int p = 0; p < np; p++) {
         a.stamps = (stp && *stp) ? c->d_stamps + (size_t)p * 8 * waves : nullptr;
         a.img = (const T *)c->d_img;
-        a.list_in = p ? c->d_list + (size_t)(p % 2) * B : nullptr;
-        a.count_in = p ? c->d_counts + (p - 1) : nullptr;
-        a.list_out = c->d_list + (size_t)((p + 1) % 2) * B;
-        a.count_out = c->d_counts + p;
+        a.list_in = p ? c->d_list + 2 * (size_t)lo + (size_t)(p % 2) * Bp : nullptr;
+        a.count_in = p ? counts + (p - 1) : nullptr;
+        a.list_out = c->d_list + 2 * (size_t)lo + (size_t)((p + 1) % 2) * Bp;
+        a.count_out = counts + p;
         a.it_state = c->d_itstate;
         a.stop_iter = stops[p];
         a.resume = p > 0;
@@ -643,7 +648,7 @@ static int launch_args(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s)
         if (p >= tail_from && c->dims.n <= 32 && c->dims.m <= 64) {
             // one QP per wave carries no idle columns: the rest of the solve is one launch
             a.stop_iter = c->set.max_iter;
-            rc = wave_launch<T>(c, a, p == 0 ? B : std::min(B, 2048), s);
+            rc = wave_launch<T>(c, a, p == 0 ? Bp : std::min(Bp, 2048), s);
             if (rc) return rc;
             np_run = p + (stp && *stp ? 1 : 0);  // (the stamps dump includes the wave launch)
             break;
@@ -665,6 +670,109 @@ static int launch_args(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s)
             std::fwrite(h.data(), 8, 8 * waves * np_run, f);
             std::fclose(f);
         }
+    }
+    return 0;
+}
+
+// Experimental (MPCQ_TILE_SCHED=queue): the whole solve as one work-queue launch (mpcq_tile.h "Work
+// queue").  Correct, but slower than the phase chains on MI355X: its device-scope counter traffic
+// (~10 atomics per 16-QP group) serialises (measured 2.9 ms vs 0.47 ms per cfg2 solve).
+template <typename T>
+static int launch_queue(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s)
+{
+    const int B = c->dims.batch;
+    int qstops[kMaxPhases];
+    const int nq = phase_stops(c->set, qstops, true);
+    a.persistent = 1;
+    a.nstages = nq;
+    for (int k = 0; k < nq; k++) a.stops[k] = qstops[k];
+    a.sched = c->d_sched;
+    a.qlist = c->d_qlist;
+    a.it_state = c->d_itstate;
+    a.img = (const T *)c->d_img;
+    a.resume = 0;
+    a.stop_iter = qstops[nq - 1];
+    if (hipMemsetAsync(c->d_sched, 0, 4 * mpcq::TileSched::kWords, s) != hipSuccess) return -2;
+    if (nq > 1 && hipMemsetAsync(c->d_qlist + B, 0, 4 * (size_t)(nq - 1) * B, s) != hipSuccess) return -2;
+    const char *stp = std::getenv("MPCQ_TILE_STAMPS");
+    const size_t waves = (size_t)(B + 15) / 16 + 4;
+    if (stp && *stp && !c->d_stamps && hipMalloc((void **)&c->d_stamps, 8 * 8 * waves * kMaxPhases) != hipSuccess)
+        return -2;
+    if (stp && *stp && hipMemsetAsync(c->d_stamps, 0, 8 * 8 * waves, s) != hipSuccess) return -2;
+    a.stamps = (stp && *stp) ? c->d_stamps : nullptr;
+    const int rc = std::is_same<T, float>::value
+                       ? mpcq_internal_tile_launch_f32((const mpcq::AdmmArgs<float> *)&a, c->KN, c->KM, s)
+                       : mpcq_internal_tile_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->KN, c->KM, s);
+    if (rc) return rc;
+    if (stp && *stp) {
+        std::vector<long long> h(8 * waves);
+        if (hipMemcpyAsync(h.data(), c->d_stamps, 8 * h.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -2;
+        if (FILE *f = std::fopen(stp, "wb")) {
+            const long long hdr[2] = {1, (long long)waves};
+            std::fwrite(hdr, 8, 2, f);
+            std::fwrite(h.data(), 8, h.size(), f);
+            std::fclose(f);
+        }
+    }
+    return 0;
+}
+
+template <typename T>
+static int launch_args(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s)
+{
+    const int B = c->dims.batch;
+    if (!c->tile) {
+        // per-plant batches: one QP per wave (operators in VGPRs); the lane kernel for shapes the wave
+        // kernel does not compile (n > 32 or m > 64) or when forced by the test hook
+        if (std::strcmp(env_kernel(), "lane") != 0 && c->dims.n <= 32 && c->dims.m <= 64) {
+            a.stop_iter = c->set.max_iter;
+            return wave_launch<T>(c, a, B, s);
+        }
+        return std::is_same<T, float>::value
+                   ? mpcq_internal_admm_launch_f32((const mpcq::AdmmArgs<float> *)&a, c->nc, c->mc, s)
+                   : mpcq_internal_admm_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->nc, c->mc, s);
+    }
+    // phases whose QPs are few (the slow tail) run one QP per wave
+    const bool all_wave = std::strcmp(env_kernel(), "wave") == 0;
+    // Small batches (under 512 tile waves) are latency-bound: one QP per wave from the start.
+    const bool small = B < 8192 && std::strcmp(env_kernel(), "tile") != 0;
+    const char *sch = std::getenv("MPCQ_TILE_SCHED");
+    c->wq_last = false;
+    if (sch && std::strcmp(sch, "queue") == 0 && !all_wave && !small) {
+        c->wq_last = true;
+        return launch_queue<T>(c, a, s);
+    }
+    // Sub-batches: the batch is cut into `split` contiguous parts, each with its own phase chain on its
+    // own stream (forked from and joined back into s).  The chains' launches overlap on the device, so
+    // the waves of one part's later, thinly populated phases fill the slots another part's phase 0
+    // leaves idle (65,536 QPs = 4,096 tile waves for 3,072 resident slots), and one part's launch
+    // fixed cost hides behind the others' work.  A QP's arithmetic does not depend on its part.
+    int split = 1;
+    if (!all_wave && !small) {
+        const char *e = std::getenv("MPCQ_TILE_SPLIT");
+        split = e ? std::atoi(e) : kDefaultSplit;
+        split = std::max(1, std::min(split, kMaxSplit));
+        while (split > 1 && B / split < 4096) split--;
+    }
+    if (split == 1) return launch_phases<T>(c, a, s, 0, B, 0, all_wave || small);
+    for (int j = 0; j < split; j++) {
+        if (j && !c->side[j] && hipStreamCreateWithFlags(&c->side[j], hipStreamNonBlocking) != hipSuccess) return -2;
+        if (!c->ev_split[j] && hipEventCreateWithFlags(&c->ev_split[j], hipEventDisableTiming) != hipSuccess) return -2;
+    }
+    if (hipEventRecord(c->ev_split[0], s) != hipSuccess) return -2;  // fork
+    for (int j = 1; j < split; j++)
+        if (hipStreamWaitEvent(c->side[j], c->ev_split[0], 0) != hipSuccess) return -2;
+    for (int j = 0; j < split; j++) {
+        const int lo = (int)((long long)B * j / split), hi = (int)((long long)B * (j + 1) / split);
+        mpcq::AdmmArgs<T> aj = a;
+        const int rc = launch_phases<T>(c, aj, j ? c->side[j] : s, lo, hi, j, false);
+        if (rc) return rc;
+    }
+    for (int j = 1; j < split; j++) {  // join
+        if (hipEventRecord(c->ev_split[j], c->side[j]) != hipSuccess) return -2;
+        if (hipStreamWaitEvent(s, c->ev_split[j], 0) != hipSuccess) return -2;
     }
     return 0;
 }
@@ -738,6 +846,11 @@ int mpcq_get_info(mpcq_ctx *c, int *status, int *iter, double *rho)
     int rc = check_ctx(c, true);
     if (rc) return rc;
     const size_t B = c->dims.batch;
+    if (c->d_sched && c->wq_last) {  // the tile work queue flags a wave that polled past its limit (never expected)
+        unsigned err = 0;
+        if ((rc = d2h(c, &err, c->d_sched + mpcq::TileSched::err(), 4))) return rc;
+        if (err) return fail(MPCQ_ERR_HIP, "tile work queue: a wave gave up polling (code " + std::to_string(err) + ")");
+    }
     if ((rc = d2h(c, status, c->d_status, 4 * B))) return rc;
     if ((rc = d2h(c, iter, c->d_iter, 4 * B))) return rc;
     return d2h(c, rho, c->d_rho, 8 * B);

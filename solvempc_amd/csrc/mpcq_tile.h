@@ -26,6 +26,10 @@
 #include <cstdlib>
 #include <type_traits>
 
+#ifndef MPCQ_REM4
+#define MPCQ_REM4 1  // build switch for A/B: 0 runs the remainder tile as a full 16x16x4 tile
+#endif
+
 namespace mpcq {
 
 template <typename T> struct Mf;
@@ -127,6 +131,12 @@ __device__ __forceinline__ int opaque(int v)
     return v;
 }
 
+// Write-through (sc1) store of data another workgroup reads within the launch (work-queue hand-off).
+template <typename V> __device__ __forceinline__ void st_sc1(V *p, V v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <typename P> __device__ __forceinline__ P fresh_ptr(P p)
 {
     int zero;
@@ -204,41 +214,81 @@ __device__ __forceinline__ void tile_mv_g(const T *__restrict__ im, const T (&x)
             for (int r = 0; r < 4; r++) y[gi][4 * t + r] = acc[gi][t][r];
 }
 
+// The 4 x 4 x 1 MFMA's partial sums of the last, 4-row tile (rem_* below) to the tile layout: lane
+// (g, c) holds p_i = sum over k = g (mod 4) of row i of the tile, for QP c; row i belongs to lane
+// group g = i.  Two lane-swap stages (v_permlane32_swap: lanes 32-63 of the first operand with lanes
+// 0-31 of the second; v_permlane16_swap: odd 16-lane rows of the first with even rows of the second)
+// sum the four partials of each row into the lanes that keep it.
+__device__ __forceinline__ float rem_reduce(const Mf<float>::acc &p)
+{
+    auto r02 = __builtin_amdgcn_permlane32_swap(__float_as_uint(p[0]), __float_as_uint(p[2]), false, false);
+    auto r13 = __builtin_amdgcn_permlane32_swap(__float_as_uint(p[1]), __float_as_uint(p[3]), false, false);
+    const float q0 = __uint_as_float(r02[0]) + __uint_as_float(r02[1]);  // rows 0 | 2 (lanes 0-31 | 32-63)
+    const float q1 = __uint_as_float(r13[0]) + __uint_as_float(r13[1]);  // rows 1 | 3
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(q0), __float_as_uint(q1), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);                // row g
+}
+
 // Products with the A operand held in VGPRs (one f32/f64 register per lane per tile and k-step: the
 // 16x16x4 A fragment, lane l = A[16 t + arow(l & 15)][4 s + (l >> 4)]), for the paired hot loop:
 // y = init + M1 x1 (+ M2 x2), the NTO x G accumulator chains interleaved k-step by k-step.
-template <typename T, int G, int NTO, int KS, int XN, bool TWO, int XN2>
+// REM (f32, n = 16 (NTO - 1) + 4, e.g. N = 20): the last tile holds 4 real rows, so it runs as
+// v_mfma_f32_4x4x1_16b (16 blocks of 4 rows x 4 QPs, one k each: a quarter of a 16x16x4's issue
+// cycles) with the A fragment lane (g, c) = A[16 (NTO - 1) + (c & 3)][4 s + g] and the iterate
+// register as B operand, then rem_reduce; its init is added after the reduction.
+template <typename T, int G, int NTO, int KS, int XN, bool TWO, int XN2, bool REM = false>
 __device__ __forceinline__ void reg_mv(const T (&m1)[NTO][KS], const T (&x1)[G][XN], const T (&m2)[NTO][KS],
                                        const T (&x2)[G][XN2], T (&y)[G][4 * NTO], const T (*init)[4 * NTO])
 {
     using A = typename Mf<T>::acc;
+    constexpr int NF = REM ? NTO - 1 : NTO;  // full 16-row tiles
+    static_assert(!REM || std::is_same<T, float>::value, "4x4x1 remainder tile: f32 only");
     A acc[G][NTO];
 #pragma unroll
     for (int gi = 0; gi < G; gi++)
 #pragma unroll
         for (int t = 0; t < NTO; t++)
 #pragma unroll
-            for (int r = 0; r < 4; r++) acc[gi][t][r] = init ? init[gi][4 * t + r] : T(0);
-#pragma unroll
-    for (int s = 0; s < KS; s++)
+            for (int r = 0; r < 4; r++) acc[gi][t][r] = (init && t < NF) ? init[gi][4 * t + r] : T(0);
+    auto step = [&](const T (&m)[NTO][KS], auto &x, int s) {
 #pragma unroll
         for (int t = 0; t < NTO; t++)
 #pragma unroll
-            for (int gi = 0; gi < G; gi++) acc[gi][t] = Mf<T>::mma(m1[t][s], x1[gi][s], acc[gi][t]);
+            for (int gi = 0; gi < G; gi++) {
+                if constexpr (REM) {
+                    if (t == NF) {
+                        acc[gi][t] = __builtin_amdgcn_mfma_f32_4x4x1f32(m[t][s], x[gi][s], acc[gi][t], 0, 0, 0);
+                        continue;
+                    }
+                }
+                acc[gi][t] = Mf<T>::mma(m[t][s], x[gi][s], acc[gi][t]);
+            }
+    };
+#pragma unroll
+    for (int s = 0; s < KS; s++) step(m1, x1, s);
     if constexpr (TWO) {
 #pragma unroll
-        for (int s = 0; s < KS; s++)
-#pragma unroll
-            for (int t = 0; t < NTO; t++)
-#pragma unroll
-                for (int gi = 0; gi < G; gi++) acc[gi][t] = Mf<T>::mma(m2[t][s], x2[gi][s], acc[gi][t]);
+        for (int s = 0; s < KS; s++) step(m2, x2, s);
     }
 #pragma unroll
     for (int gi = 0; gi < G; gi++)
 #pragma unroll
         for (int t = 0; t < NTO; t++)
 #pragma unroll
-            for (int r = 0; r < 4; r++) y[gi][4 * t + r] = acc[gi][t][r];
+            for (int r = 0; r < 4; r++) {
+                if constexpr (REM) {
+                    if (t == NF) {
+                        if (r == 0) {
+                            const T v = rem_reduce(acc[gi][t]);
+                            y[gi][4 * t] = init ? v + init[gi][4 * t] : v;
+                        } else {
+                            y[gi][4 * t + r] = T(0);
+                        }
+                        continue;
+                    }
+                }
+                y[gi][4 * t + r] = acc[gi][t][r];
+            }
 }
 
 // G: 16-QP groups per wave; OCC: waves per SIMD the register allocation is held to (256-thread
@@ -343,17 +393,9 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
     MPCQ_TSTAMP(1, (long long)__builtin_amdgcn_s_memtime());
 
     const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-    const int wave_slot = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 * G;
-    if (wave_slot >= count) return;
     constexpr int KNR = PAIRED ? KN : 1, NTR = PAIRED ? NT : 1;
-    bool valid[G];
-    int b_[G];
-#pragma unroll
-    for (int gi = 0; gi < G; gi++) {
-        const int slot = wave_slot + 16 * gi + c;
-        valid[gi] = slot < count;
-        b_[gi] = valid[gi] ? (a.list_in ? a.list_in[slot] : slot) : 0;
-    }
+    // f32 paired loop with n = 16 (NT - 1) + 4 (N = 20): the last tile's 4 rows on the 4x4x1 MFMA
+    constexpr bool REM4 = PAIRED && std::is_same<T, float>::value && KN % 4 == 1 && NT > 1 && MPCQ_REM4;
     const int n = a.n, m = a.m;
     const int ncs = NCP, mcs = MCP;                // state row strides (ctx nc, mc)
     const PlantOps<T> op = a.ops;                  // shared plant: block 0
@@ -361,6 +403,22 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
     const SolverSettings &st = a.st;
     const bool scaled_term = st.scaled_termination != 0;
     const double c64 = (double)op.cs[0];
+    const bool persist = a.persistent != 0;
+    // work queue: this workgroup's shard of the batch, QPs [sh_lo, sh_hi)
+    const unsigned B = (unsigned)a.batch;
+    const unsigned nsh = gridDim.x < (unsigned)TileSched::kShards ? gridDim.x : (unsigned)TileSched::kShards;
+    const unsigned shard = blockIdx.x % nsh;
+    const unsigned sh_lo = (unsigned)((unsigned long long)B * shard / nsh);
+    const unsigned sh_hi = (unsigned)((unsigned long long)B * (shard + 1) / nsh);
+
+    // One group of 16 G QPs (column c of group gi: QP b_[gi], live if valid[gi]) from the start of
+    // `stage` to its stop iteration (work queue), or of this launch's phase (phase schedule).
+    auto run_group = [&](const int (&b_)[G], const bool (&valid)[G], const int stage) {
+    // lane indices re-derived opaquely per group, so that no lane-dependent address of the body is
+    // hoisted out of the work-queue loop and held live (in VGPRs) across the hot loop
+    const int lane = opaque((int)threadIdx.x & 63), c = lane & 15, g = lane >> 4;
+    const bool resume = persist ? stage > 0 : a.resume != 0;
+    const bool mpc_fe = persist ? (stage == 0 && a.mpc) : a.mpc != 0;  // front end: the QP's first stage
 
     // ---- per-QP data (element v = 4 s + g of this lane's QP column), per group.  Every global load
     // of a group is issued (index clamped into the row, not branched) before any of it is used.
@@ -372,7 +430,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
     for (int gi = 0; gi < G; gi++) {
         const int b = b_[gi];
         double qk[KN], up[KM], lo[LFREE ? 1 : KM];
-        if (a.mpc) {  // setF (:372-375) q = Fx X + Fu U + Fr ref;  (:93-99) u = W0 + Sbar X + Ku U
+        if (mpc_fe) {  // setF (:372-375) q = Fx X + Fu U + Fr ref;  (:93-99) u = W0 + Sbar X + Ku U
             double Xv[8];
             const int nx = a.nx;
 #pragma unroll
@@ -390,7 +448,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
                     if (t < nx) s0 += fe[FE_FX + 8 * v + t] * Xv[t];
                 const double s1 = fe[FE_FU + v] * Uv;
                 qk[s] = s0 + s1 + fe[FE_FR + v];
-                if (valid[gi] && v < n) a.q_out[(size_t)b * n + v] = qk[s];
+                if (valid[gi] && v < n) st_sc1(a.q_out + (size_t)b * n + v, qk[s]);  // read by later stages
             }
 #pragma unroll
             for (int s = 0; s < KM; s++) {
@@ -400,7 +458,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
                 for (int t = 0; t < 8; t++)
                     if (t < nx) sx += fe[FE_SB + 8 * v + t] * Xv[t];
                 up[s] = fe[FE_W0 + v] + sx + fe[FE_KU + v] * Uv;
-                if (valid[gi] && v < m) a.u_out[(size_t)b * m + v] = up[s];
+                if (valid[gi] && v < m) st_sc1(a.u_out + (size_t)b * m + v, up[s]);
             }
         } else {
 #pragma unroll
@@ -435,7 +493,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
                 const double e = fe[FE_E + v];  // osqp_update_bounds: u^ = E u, l^ = E l
                 uu = up[s] * e;
                 if constexpr (!LFREE) ll = lo[s] * e;
-                if (!a.resume) {  // a resumed phase's QPs passed these checks in phase 0
+                if (!resume) {  // a resumed phase's QPs passed these checks in phase 0
                     if (uu < ll) bad = 1;
                     if constexpr (ALL_INEQ && LFREE) {
                         if (uu > kInfty * kMinScaling) tchg = 1;  // a free row: not the setup's type
@@ -467,11 +525,11 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
     T xs[G][NS], z[G][MS], y[G][MS];
     T rho[G], rinv[G];
     int it = 0;
-    const bool load_state = a.resume || (a.warm && !a.fresh);
+    const bool load_state = resume || (a.warm && !a.fresh);
 #pragma unroll
     for (int gi = 0; gi < G; gi++) {
         const int b = b_[gi];
-        if (a.resume) {
+        if (resume) {
             rho[gi] = a.rhos[b];
             if (gi == 0) it = a.it_state[b];
         } else {
@@ -571,7 +629,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
 
     const int ct = st.check_termination;
     const int ai = (st.adaptive_rho && a.adaptive_interval) ? a.adaptive_interval : 0;
-    const int stop = a.stop_iter;
+    const int stop = persist ? a.stops[stage] : a.stop_iter;
     int next_check = ct ? (it / ct + 1) * ct : -1;  // uniform; no integer division in the loop
     int next_adapt = ai ? (it / ai + 1) * ai : -1;
     T dx[G][NS], dy[G][MS];
@@ -579,13 +637,17 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
     auto load_regs = [&](T (&rS)[NTR][KNR], T (&rBt)[NTR][KNR], T (&rB)[NTR][KNR]) {
         const T *im = fresh_ptr((const T *)img);
 #pragma unroll
-        for (int t = 0; t < NTR; t++)
+        for (int t = 0; t < NTR; t++) {
+            // REM4: the 4x4x1 tile's fragment lane (g, c) is the 16x16x4 image's lane (g, 4 (c & 3))
+            // (image row i holds logical row arow(i) = 4 (i & 3) + (i >> 2))
+            const int ln = (REM4 && t == NTR - 1) ? ((lane & 48) | ((lane & 3) << 2)) : lane;
 #pragma unroll
             for (int k = 0; k < KNR; k++) {
-                rS[t][k] = im[L.S + TileLayout::at(KNP, VEC, t, k, lane)];
-                rBt[t][k] = im[L.Bt + TileLayout::at(KMP, VEC, t, k, lane)];
-                rB[t][k] = im[L.B + TileLayout::at(KNP, VEC, t, k, lane)];
+                rS[t][k] = im[L.S + TileLayout::at(KNP, VEC, t, k, ln)];
+                rBt[t][k] = im[L.Bt + TileLayout::at(KMP, VEC, t, k, ln)];
+                rB[t][k] = im[L.B + TileLayout::at(KNP, VEC, t, k, ln)];
             }
+        }
     };
     // one paired ADMM iteration (see the PAIRED note above the kernel)
     auto piter = [&](auto with_delta, const T (&rS)[NTR][KNR], const T (&rBt)[NTR][KNR], const T (&rB)[NTR][KNR]) {
@@ -599,7 +661,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
                 for (int s = 0; s < KN; s++)
                     wt[gi][s] = tt_fma(rho[gi], z[gi][s], -y[gi][s]) - tt_fma(rho[gi], z[gi][s + KN], -y[gi][s + KN]);
             T xi[G][NS];
-            reg_mv<T, G, NT, KN, NS, true>(rS, xs, rBt, wt, xi, gv);
+            reg_mv<T, G, NT, KN, NS, true, KNR, REM4>(rS, xs, rBt, wt, xi, gv);
 #pragma unroll
             for (int gi = 0; gi < G; gi++)
 #pragma unroll
@@ -611,7 +673,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
                 }
             // z~_top = B~ eta (z~_bot = -z~_top) ; relaxation ; projection ; dual update
             T zt[G][NS];
-            reg_mv<T, G, NT, KN, NS, false>(rB, xi, rB, wt, zt, nullptr);
+            reg_mv<T, G, NT, KN, NS, false, KNR, REM4>(rB, xi, rB, wt, zt, nullptr);
 #pragma unroll
             for (int gi = 0; gi < G; gi++)
 #pragma unroll
@@ -648,7 +710,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
                 for (int s = 0; s < KN; s++)
                     wt[gi][s] = rho[gi] * ((z[gi][s] - y[gi][s]) - (z[gi][s + KN] - y[gi][s + KN]));
             T xi[G][NS];
-            reg_mv<T, G, NT, KN, KNR, false>(rBt, wt, rBt, wt, xi, sx);  // xi = (-g + S x') + B~' w~
+            reg_mv<T, G, NT, KN, KNR, false, KNR, REM4>(rBt, wt, rBt, wt, xi, sx);  // xi = (-g + S x') + B~' w~
 #pragma unroll
             for (int gi = 0; gi < G; gi++)
 #pragma unroll
@@ -657,8 +719,8 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
                     xs[gi][s] = tt_fma(oma, xs[gi][s], xi[gi][s]);  // x' = alpha eta + (1 - alpha) x'
                 }
             T zt[G][NS];
-            reg_mv<T, G, NT, KN, NS, false>(rB, xi, rB, wt, zt, nullptr);  // alpha z~_top = B~ eta'
-            reg_mv<T, G, NT, KN, NS, false>(rS, xs, rS, wt, sx, gv);       // next: -g + S x'
+            reg_mv<T, G, NT, KN, NS, false, KNR, REM4>(rB, xi, rB, wt, zt, nullptr);  // alpha z~_top = B~ eta'
+            reg_mv<T, G, NT, KN, NS, false, KNR, REM4>(rS, xs, rS, wt, sx, gv);       // next: -g + S x'
 #pragma unroll
             for (int gi = 0; gi < G; gi++)
 #pragma unroll
@@ -671,7 +733,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
                 }
         }
     };
-    MPCQ_TSTAMP(2, (long long)__builtin_amdgcn_s_memtime());
+    if (!persist) MPCQ_TSTAMP(2, (long long)__builtin_amdgcn_s_memtime());
     while (!all_done()) {
         if constexpr (PAIRED) {
             // plain iterations up to the next info iteration, with the operators held in VGPRs
@@ -683,7 +745,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
                 T rS[NTR][KNR], rBt[NTR][KNR], rB[NTR][KNR];
                 load_regs(rS, rBt, rB);
                 T sx[G][NS], adk[G][KNR];
-                reg_mv<T, G, NT, KN, NS, false>(rS, xs, rS, xs, sx, gv);
+                reg_mv<T, G, NT, KN, NS, false, NS, REM4>(rS, xs, rS, xs, sx, gv);
 #pragma unroll
                 for (int gi = 0; gi < G; gi++) {
 #pragma unroll
@@ -1037,8 +1099,11 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
             for (int gi = 0; gi < G; gi++) done[gi] = term[gi];
         }
         if (it == stop && !all_done()) {
-            MPCQ_TSTAMP(3, (long long)__builtin_amdgcn_s_memtime());
-            // phase boundary: save the running QPs and queue them for the next launch
+            if (!persist) MPCQ_TSTAMP(3, (long long)__builtin_amdgcn_s_memtime());
+            // stage / phase boundary: save the running QPs and queue them for the next stage / launch.
+            // Work queue: the state is another workgroup's input within this launch, so it is stored
+            // write-through (sc1) and drained before the queue entries (the flags) are written
+            // (cdna_hip_programming.md G16 recipe R1; the consumer polls the entries, then acquires).
 #pragma unroll
             for (int gi = 0; gi < G; gi++) {
                 const bool run = !done[gi];
@@ -1046,30 +1111,192 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
                 if (run) {
 #pragma unroll
                     for (int s = 0; s < NS; s++)
-                        if (s < KN) a.xs[(size_t)b * ncs + 4 * s + g] = xs[gi][s];
+                        if (s < KN) st_sc1(a.xs + (size_t)b * ncs + 4 * s + g, xs[gi][s]);
 #pragma unroll
                     for (int s = 0; s < MS; s++)
                         if (s < KM) {
-                            a.zs[(size_t)b * mcs + 4 * s + g] = z[gi][s];
-                            a.ys[(size_t)b * mcs + 4 * s + g] = y[gi][s];
+                            st_sc1(a.zs + (size_t)b * mcs + 4 * s + g, z[gi][s]);
+                            st_sc1(a.ys + (size_t)b * mcs + 4 * s + g, y[gi][s]);
                         }
                     if (g == 0) {
-                        a.rhos[b] = rho[gi];
-                        a.it_state[b] = it;
+                        st_sc1(a.rhos + b, rho[gi]);
+                        st_sc1(a.it_state + b, it);
                     }
                 }
-                const unsigned long long mask = __ballot(run && g == 0);
-                int base = 0;
-                if (lane == 0 && mask) base = atomicAdd(a.count_out, __popcll(mask));
-                base = __shfl(base, 0);
-                if (run && g == 0) a.list_out[base + __popcll(mask & ((1ull << lane) - 1ull))] = b;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            unsigned long long mask[G];
+            unsigned total = 0;
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                mask[gi] = __ballot(!done[gi] && g == 0);
+                total += (unsigned)__popcll(mask[gi]);
+            }
+            int base = 0;
+            if (lane == 0)
+                base = persist ? (int)__hip_atomic_fetch_add(a.sched + TileSched::res(stage + 1, shard), total,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : atomicAdd(a.count_out, (int)total);
+            base = __shfl(base, 0);
+            int *const qout = persist ? a.qlist + (size_t)(stage + 1) * a.batch + sh_lo : a.list_out;
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                const unsigned long long below = (1ull << lane) - 1ull;
+                int pos = base + __popcll(mask[gi] & below);
+#pragma unroll
+                for (int gj = 0; gj < gi; gj++) pos += __popcll(mask[gj]);
+                if (!done[gi] && g == 0) {
+                    const int b = opaque(b_[gi]);
+                    if (persist) st_sc1(qout + pos, b + 1);  // the flag a consumer polls
+                    else qout[pos] = b;
+                }
             }
             break;
         }
     }
+    if (!persist) MPCQ_TSTAMP(5, (long long)it);
+    };  // run_group
+
+    // ---- Work queue (one launch per solve).  After each group a wave claims 16 G QPs of its shard:
+    // fresh QPs of stage 0 first (they carry the most remaining work), else a full group of the
+    // lowest continuation stage that has one, else the remainder of the lowest non-empty stage; it
+    // leaves when its shard has nothing queued.  Nothing is orphaned: a wave that hands QPs on claims
+    // again afterwards, so the last wave of a shard drains its queues.  Claims are atomic (fetch-add
+    // on the fresh counter, compare-and-swap on a stage's tak); no wave ever waits for work.  The
+    // phase schedule runs the loop once, on the wave's slots of the launch's list.  (One call site:
+    // run_group is inlined once.)
+    unsigned *const S = a.sched;
+    const unsigned NSTG = (unsigned)a.nstages;
+    constexpr unsigned WANT = 16 * G;
+    constexpr unsigned kMaxPolls = 1u << 21;
+    auto ld = [](const unsigned *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    bool first = true, fresh_left = true;
+    long long st_groups = 0, st_qps = 0, st_busy = 0;  // debug stamps (work queue): groups, QPs, cycles in groups
+    for (;;) {
+        int k = -2;
+        unsigned base = 0, cnt = 0;
+        if (!persist) {
+            // phase schedule: this wave's 16 G QPs are slots wave_slot.. of the launch's list
+            const int wave_slot = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 * G;
+            if (!first || wave_slot >= count) break;
+            k = 0;
+            base = (unsigned)wave_slot;
+            cnt = (unsigned)(count - wave_slot);
+        } else if (lane == 0) {
+            const unsigned nfresh = sh_hi - sh_lo;
+            if (fresh_left) {
+                const unsigned t = __hip_atomic_fetch_add(S + TileSched::tak(0, shard), WANT, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                if (t < nfresh) { k = 0; base = sh_lo + t; cnt = nfresh - t < WANT ? nfresh - t : WANT; }
+                else fresh_left = false;
+            }
+            for (int tries = 0; k == -2 && tries < 64; tries++) {
+                unsigned res[kMaxStages], tak[kMaxStages];
+#pragma unroll
+                for (int s = 1; s < kMaxStages; s++)
+                    if (s < (int)NSTG) {
+                        res[s] = ld(S + TileSched::res(s, shard));
+                        tak[s] = ld(S + TileSched::tak(s, shard));
+                    }
+                int pick = -1;
+                unsigned p_res = 0, p_tak = 0;  // (no runtime-indexed arrays: they would live in scratch)
+#pragma unroll
+                for (int s = kMaxStages - 1; s >= 1; s--)  // lowest full stage, else lowest non-empty
+                    if (s < (int)NSTG && res[s] > tak[s] &&
+                        (pick < 0 || res[s] - tak[s] >= WANT || p_res - p_tak < WANT)) {
+                        pick = s;
+                        p_res = res[s];
+                        p_tak = tak[s];
+                    }
+                if (pick < 0) { k = -1; break; }  // the shard has nothing queued: leave
+                const unsigned avail = p_res - p_tak, want = avail < WANT ? avail : WANT;
+                unsigned expect = p_tak;
+                if (__hip_atomic_compare_exchange_strong(S + TileSched::tak(pick, shard), &expect, p_tak + want,
+                                                         __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    k = pick; base = p_tak; cnt = want;
+                }
+            }
+            if (k == -2) k = -1;  // 64 lost races in a row: leave (the winners drain the queue)
+        }
+        first = false;
+        k = __builtin_amdgcn_readfirstlane(k);
+        base = __builtin_amdgcn_readfirstlane(base);
+        cnt = __builtin_amdgcn_readfirstlane(cnt);
+        fresh_left = __builtin_amdgcn_readfirstlane((int)fresh_left) != 0;
+        if (k < 0) break;
+        bool valid[G];
+        int b_[G];
+        if (k == 0) {
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                const unsigned slot = 16 * gi + c;
+                valid[gi] = slot < cnt;
+                const int i = (int)(base + slot);
+                b_[gi] = valid[gi] ? (a.list_in ? a.list_in[i] : a.qp0 + i) : 0;
+            }
+        } else {
+            // the entries were reserved before this claim; poll until their producers wrote them
+            const int *q = a.qlist + (size_t)k * B + sh_lo + base;
+            bool ok = false;
+            for (unsigned sp = 0; sp < kMaxPolls; sp++) {
+                bool all = true;
+#pragma unroll
+                for (int gi = 0; gi < G; gi++) {
+                    const unsigned slot = 16 * gi + c;
+                    valid[gi] = slot < cnt;
+                    b_[gi] = valid[gi] ? __hip_atomic_load(q + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1 : 0;
+                    all = all && (!valid[gi] || b_[gi] >= 0);
+                }
+                if (wave_all(all)) { ok = true; break; }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (!ok) {
+                if (lane == 0) __hip_atomic_store(S + TileSched::err(), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            // acquire: the state behind the entries (stored sc1 and drained by their producers)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const long long t_run = a.stamps ? (long long)__builtin_amdgcn_s_memtime() : 0;
+        run_group(b_, valid, k);
+        if (a.stamps) {
+            st_groups++;
+            st_qps += cnt;
+            st_busy += (long long)__builtin_amdgcn_s_memtime() - t_run;
+        }
+    }
+    if (persist) {
+        MPCQ_TSTAMP(2, st_groups);
+        MPCQ_TSTAMP(3, st_qps);
+        MPCQ_TSTAMP(5, st_busy);
+    }
     MPCQ_TSTAMP(4, (long long)__builtin_amdgcn_s_memtime());
-    MPCQ_TSTAMP(5, (long long)it);
     MPCQ_TSTAMP(7, (long long)__builtin_amdgcn_s_memrealtime());
+}
+
+// Launch one tile-kernel variant: one workgroup per 64 G QPs (phase schedule), or for the work
+// queue at most as many workgroups as are resident at once (the kernel's occupancy x CUs, cached per
+// variant), each looping over claimed groups.
+template <typename T, int KN, int KM, bool AI, bool LF, int G, int OCC, bool PAIRED = false>
+int tile_launch_variant(const AdmmArgs<T> &a, hipStream_t s)
+{
+    auto kern = admm_tile_kernel<T, KN, KM, AI, LF, G, OCC, PAIRED>;
+    int blocks = (a.batch + 64 * G - 1) / (64 * G);
+    if (a.persistent) {
+        static int resident = 0;
+        if (!resident) {
+            int per_cu = 0, dev = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess ||
+                hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu < 1)
+                return -2;
+            resident = per_cu * cus;
+        }
+        blocks = blocks < resident ? blocks : resident;
+    }
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 // occ: 0 = default for the shape/type, else a requested variant (benchmark A/B hook):
@@ -1077,39 +1304,27 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
 template <typename T, int KN, int KM>
 int tile_launch(const AdmmArgs<T> &a, int occ, hipStream_t s)
 {
-    const dim3 block(256);
-    auto grid = [&](int G) { return dim3((a.batch + 64 * G - 1) / (64 * G)); };
     if constexpr (KM == 2 * KN) {
         if (a.paired && a.all_ineq && a.lower_free) {  // the condensed-MPC shape: paired, VGPR-resident loop
             if constexpr (sizeof(T) == 8) {
-                hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 1, 2, true>), grid(1), block, 0, s, a);
+                return tile_launch_variant<T, KN, KM, true, true, 1, 2, true>(a, s);
             } else {
-                if (occ == 2)
-                    hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 2, 2, true>), grid(2), block, 0, s, a);
-                else if (occ == 4)
-                    hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 1, 4, true>), grid(1), block, 0, s, a);
-                else
-                    hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 1, 3, true>), grid(1), block, 0, s, a);
+                if (occ == 2) return tile_launch_variant<T, KN, KM, true, true, 2, 2, true>(a, s);
+                if (occ == 4) return tile_launch_variant<T, KN, KM, true, true, 1, 4, true>(a, s);
+                return tile_launch_variant<T, KN, KM, true, true, 1, 3, true>(a, s);
             }
-            return hipGetLastError() == hipSuccess ? 0 : -2;
         }
     }
     if (a.all_ineq && a.lower_free) {
         if constexpr (sizeof(T) == 8) {
-            if (occ == 1)
-                hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 2, 1>), grid(2), block, 0, s, a);
-            else
-                hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 1, 2>), grid(1), block, 0, s, a);
+            if (occ == 1) return tile_launch_variant<T, KN, KM, true, true, 2, 1>(a, s);
+            return tile_launch_variant<T, KN, KM, true, true, 1, 2>(a, s);
         } else {
-            if (occ == 2)
-                hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 2, 2>), grid(2), block, 0, s, a);
-            else
-                hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 1, 3>), grid(1), block, 0, s, a);
+            if (occ == 2) return tile_launch_variant<T, KN, KM, true, true, 2, 2>(a, s);
+            return tile_launch_variant<T, KN, KM, true, true, 1, 3>(a, s);
         }
-    } else {
-        hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, false, false, 1, 2>), grid(1), block, 0, s, a);
     }
-    return hipGetLastError() == hipSuccess ? 0 : -2;
+    return tile_launch_variant<T, KN, KM, false, false, 1, 2>(a, s);
 }
 
 // Compiled (KN, KM) = (ceil(n/4), ceil(m/4)): the reference horizons N = 15 (n 15, m 30) and N = 20

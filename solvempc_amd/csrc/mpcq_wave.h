@@ -466,7 +466,7 @@ __global__ __launch_bounds__(64, 2) void admm_wave_kernel(AdmmArgs<T> a, int nc,
     __shared__ __attribute__((aligned(16))) T bcw[BM];  // row-side broadcast (w, y, d)
     const int count = a.count_in ? *a.count_in : a.batch;
     for (int slot = blockIdx.x; slot < count; slot += gridDim.x)  // uniform: one wave per block
-        wave_solve_one<T, NCAP, MCAP, ALL_INEQ, LFREE>(a, nc, mc, a.list_in ? a.list_in[slot] : slot, bcx, bcw);
+        wave_solve_one<T, NCAP, MCAP, ALL_INEQ, LFREE>(a, nc, mc, a.list_in ? a.list_in[slot] : a.qp0 + slot, bcx, bcw);
 }
 
 
