@@ -35,8 +35,6 @@ int fail(int code, const std::string &msg)
     } while (0)
 
 constexpr int kMaxPhases = 16;
-constexpr int kMaxSplit = 8;      // tile sub-batch chains (streams) per solve
-constexpr int kDefaultSplit = 1;  // measured: 4 parts on 4 streams ran no faster (0.52 vs 0.47 ms per cfg2 solve)
 
 size_t setup_scratch_len(int n, int m)
 {
@@ -59,8 +57,6 @@ struct mpcq_ctx {
     unsigned *d_sched = nullptr;  // tile work queue: TileSched counters
     int *d_qlist = nullptr;       //                  [stage][batch] queue entries
     bool wq_last = false;         // the last solve ran the work queue (its error word is valid)
-    hipStream_t side[kMaxSplit] = {};     // tile sub-batch streams (side[0] unused: part 0 runs on the caller's)
-    hipEvent_t ev_split[kMaxSplit] = {};  // fork (0) / join (j) events of the sub-batch chains
     long long *d_stamps = nullptr;  // debug (MPCQ_TILE_STAMPS)
     hipStream_t last = nullptr;
     int nx = 0;
@@ -347,8 +343,9 @@ int mpcq_create(const mpcq_dims *d, const mpcq_settings *s, mpcq_ctx **out)
     if (tile) {
         const mpcq::TileLayout TL = mpcq::TileLayout::make(KN, KM, (int)(16 / es));
         A(&c->d_img, es * TL.total);
-        A((void **)&c->d_list, 4 * 2 * B);
-        A((void **)&c->d_counts, 4 * kMaxPhases * kMaxSplit);
+        const size_t lcap = (size_t)mpcq::ListSeg::kShards * mpcq::ListSeg::cap(B);  // entries per phase list
+        A((void **)&c->d_list, 4 * 2 * lcap);
+        A((void **)&c->d_counts, 4 * kMaxPhases * mpcq::ListSeg::kCounters);
         A((void **)&c->d_itstate, 4 * B);
         A((void **)&c->d_sched, 4 * mpcq::TileSched::kWords);
         A((void **)&c->d_qlist, 4 * (size_t)mpcq::kMaxStages * B);
@@ -376,10 +373,6 @@ int mpcq_destroy(mpcq_ctx *c)
                     c->d_Sbar, c->d_Ku, c->d_W0, c->d_X, c->d_U, c->d_img, c->d_list, c->d_counts,
                     c->d_itstate, c->d_Ad, c->d_Bd, c->d_step, c->d_flags, c->d_stamps, c->d_mimo, c->d_sched, c->d_qlist};
     if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
-    for (int j = 0; j < kMaxSplit; j++) {
-        if (c->side[j]) (void)hipStreamDestroy(c->side[j]);
-        if (c->ev_split[j]) (void)hipEventDestroy(c->ev_split[j]);
-    }
     if (c->graph) (void)hipGraphDestroy(c->graph);
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
@@ -609,53 +602,54 @@ static int wave_launch(mpcq_ctx *c, const mpcq::AdmmArgs<T> &a, int grid, hipStr
                : mpcq_internal_wave_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->nc, c->mc, grid, s);
 }
 
-// The phase chain of QPs [lo, hi) of a tile context on stream s (part `part` of the batch: its own
-// two alternating QP lists in d_list[2 lo, 2 hi) and its own phase counters).
+// The phase chain of a tile solve on stream s: phase p's QPs still running at its stop are appended to
+// the ListSeg list of phase p + 1 (two alternating lists; each phase its own block of counters).
 template <typename T>
-static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, int lo, int hi, int part, bool wave_only)
+static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool wave_only)
 {
-    const int Bp = hi - lo;
+    const int B = c->dims.batch;
     int stops[kMaxPhases];
     const int np = phase_stops(c->set, stops);
-    int *const counts = c->d_counts + (size_t)part * kMaxPhases;
-    if (hipMemsetAsync(counts, 0, 4 * kMaxPhases, s) != hipSuccess) return -2;
+    const int seg = mpcq::ListSeg::cap(B);
+    const size_t lcap = (size_t)mpcq::ListSeg::kShards * seg;
+    if (hipMemsetAsync(c->d_counts, 0, 4 * (size_t)np * mpcq::ListSeg::kCounters, s) != hipSuccess) return -2;
     const int mpc = a.mpc;
     const char *te = std::getenv("MPCQ_TAIL_PHASE");
     const int tail_from = wave_only ? 0 : (te ? std::atoi(te) : 3);
     int np_run = 0;
-    a.batch = Bp;
-    a.qp0 = lo;
+    a.list_seg = seg;
 
-    // debug hook (one part only): per-wave stage stamps of every phase launch, written to
-    // $MPCQ_TILE_STAMPS after the solve
-    const char *stp = part == 0 ? std::getenv("MPCQ_TILE_STAMPS") : nullptr;
-    const size_t waves = (size_t)(Bp + 15) / 16 + 4;
+    // debug hook: per-wave stage stamps of every phase launch, written to $MPCQ_TILE_STAMPS after the solve
+    const char *stp = std::getenv("MPCQ_TILE_STAMPS");
+    const size_t waves = (size_t)(B + 15) / 16 + 4 * mpcq::ListSeg::kShards;
     if (stp && *stp && !c->d_stamps && hipMalloc((void **)&c->d_stamps, 8 * 8 * waves * kMaxPhases) != hipSuccess)
         return -2;
     if (stp && *stp && hipMemsetAsync(c->d_stamps, 0, 8 * 8 * waves * kMaxPhases, s) != hipSuccess) return -2;
     for (int p = 0; p < np; p++) {
         a.stamps = (stp && *stp) ? c->d_stamps + (size_t)p * 8 * waves : nullptr;
         a.img = (const T *)c->d_img;
-        a.list_in = p ? c->d_list + 2 * (size_t)lo + (size_t)(p % 2) * Bp : nullptr;
-        a.count_in = p ? counts + (p - 1) : nullptr;
-        a.list_out = c->d_list + 2 * (size_t)lo + (size_t)((p + 1) % 2) * Bp;
-        a.count_out = counts + p;
+        a.list_in = p ? c->d_list + (size_t)(p % 2) * lcap : nullptr;
+        a.count_in = p ? c->d_counts + (size_t)(p - 1) * mpcq::ListSeg::kCounters : nullptr;
+        a.list_out = c->d_list + (size_t)((p + 1) % 2) * lcap;
+        a.count_out = c->d_counts + (size_t)p * mpcq::ListSeg::kCounters;
         a.it_state = c->d_itstate;
         a.stop_iter = stops[p];
         a.resume = p > 0;
         a.mpc = p == 0 ? mpc : 0;  // later phases read q, u from the buffers phase 0 filled
         int rc;
         if (p >= tail_from && c->dims.n <= 32 && c->dims.m <= 64) {
-            // one QP per wave carries no idle columns: the rest of the solve is one launch
+            // one QP per wave carries no idle columns: the rest of the solve is one launch (a resumed
+            // list: a multiple of ListSeg::kShards blocks)
             a.stop_iter = c->set.max_iter;
-            rc = wave_launch<T>(c, a, p == 0 ? Bp : std::min(Bp, 2048), s);
+            rc = wave_launch<T>(c, a, p == 0 ? B : 2048, s);
             if (rc) return rc;
             np_run = p + (stp && *stp ? 1 : 0);  // (the stamps dump includes the wave launch)
             break;
-        } else
-            rc = std::is_same<T, float>::value
-                     ? mpcq_internal_tile_launch_f32((const mpcq::AdmmArgs<float> *)&a, c->KN, c->KM, s)
-                     : mpcq_internal_tile_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->KN, c->KM, s);
+        }
+        // every phase launches the phase-0 grid: list segment s is served by the blocks b % kShards == s
+        rc = std::is_same<T, float>::value
+                 ? mpcq_internal_tile_launch_f32((const mpcq::AdmmArgs<float> *)&a, c->KN, c->KM, s)
+                 : mpcq_internal_tile_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->KN, c->KM, s);
         if (rc) return rc;
         np_run = p + 1;
     }
@@ -744,37 +738,7 @@ static int launch_args(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s)
         c->wq_last = true;
         return launch_queue<T>(c, a, s);
     }
-    // Sub-batches: the batch is cut into `split` contiguous parts, each with its own phase chain on its
-    // own stream (forked from and joined back into s).  The chains' launches overlap on the device, so
-    // the waves of one part's later, thinly populated phases fill the slots another part's phase 0
-    // leaves idle (65,536 QPs = 4,096 tile waves for 3,072 resident slots), and one part's launch
-    // fixed cost hides behind the others' work.  A QP's arithmetic does not depend on its part.
-    int split = 1;
-    if (!all_wave && !small) {
-        const char *e = std::getenv("MPCQ_TILE_SPLIT");
-        split = e ? std::atoi(e) : kDefaultSplit;
-        split = std::max(1, std::min(split, kMaxSplit));
-        while (split > 1 && B / split < 4096) split--;
-    }
-    if (split == 1) return launch_phases<T>(c, a, s, 0, B, 0, all_wave || small);
-    for (int j = 0; j < split; j++) {
-        if (j && !c->side[j] && hipStreamCreateWithFlags(&c->side[j], hipStreamNonBlocking) != hipSuccess) return -2;
-        if (!c->ev_split[j] && hipEventCreateWithFlags(&c->ev_split[j], hipEventDisableTiming) != hipSuccess) return -2;
-    }
-    if (hipEventRecord(c->ev_split[0], s) != hipSuccess) return -2;  // fork
-    for (int j = 1; j < split; j++)
-        if (hipStreamWaitEvent(c->side[j], c->ev_split[0], 0) != hipSuccess) return -2;
-    for (int j = 0; j < split; j++) {
-        const int lo = (int)((long long)B * j / split), hi = (int)((long long)B * (j + 1) / split);
-        mpcq::AdmmArgs<T> aj = a;
-        const int rc = launch_phases<T>(c, aj, j ? c->side[j] : s, lo, hi, j, false);
-        if (rc) return rc;
-    }
-    for (int j = 1; j < split; j++) {  // join
-        if (hipEventRecord(c->ev_split[j], c->side[j]) != hipSuccess) return -2;
-        if (hipStreamWaitEvent(s, c->ev_split[j], 0) != hipSuccess) return -2;
-    }
-    return 0;
+    return launch_phases<T>(c, a, s, all_wave || small);
 }
 
 template <typename T>

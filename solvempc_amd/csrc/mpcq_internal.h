@@ -125,6 +125,19 @@ struct TileSched {
     static constexpr int kWords = (kShards * kMaxStages * 2 + 1) * kStride;
 };
 
+// Phase lists of the tile path: the QPs a phase hands on are appended to one of kShards segments
+// (the appending workgroup's blockIdx % kShards), each with its own counter on its own 128-B line, so
+// the ~3,000 waves reaching a phase boundary together do not serialise on one device-scope counter
+// (~11 ns per atomic).  Segment s holds entries [s cap, s cap + count[s * kStride]).  The next phase's
+// workgroup b serves segment b % kShards (its 64 G slots at (b / kShards) 64 G): the workgroups of a
+// segment are exactly those that can have filled it, so every entry is covered.
+struct ListSeg {
+    static constexpr int kShards = 32;
+    static constexpr int kStride = 32;  // ints per counter line
+    static constexpr int kCounters = kShards * kStride;
+    __host__ __device__ static constexpr int cap(int batch) { return (batch + kShards - 1) / kShards + 256; }
+};
+
 // Arguments of the ADMM kernel (one QP per lane).
 template <typename T>
 struct AdmmArgs {
@@ -158,9 +171,10 @@ struct AdmmArgs {
     int mpc_u;                  // U += x[0] at termination (the front end may have run in an earlier phase)
     // tile kernel (shared plant): MFMA operand images and the phase machinery (mpcq_tile.h)
     const T *img;               // TileLayout images of the plant
-    const int *list_in;         // active QP indices of this phase (null: identity 0..batch-1)
-    const int *count_in;        // device count of list_in (null: batch)
-    int *list_out, *count_out;  // QPs still running at stop_iter (appended)
+    const int *list_in;         // active QP indices of this phase (null: identity 0..batch-1), ListSeg layout
+    const int *count_in;        // ListSeg counters of list_in (null: batch)
+    int *list_out, *count_out;  // QPs still running at stop_iter (appended, ListSeg layout)
+    int list_seg;               // ListSeg segment capacity
     int *it_state;              // [batch] iterations done so far in this solve
     int qp0;                    // QP index of identity-list slot 0 (sub-batch parts of a tile solve)
     int stop_iter;              // phase boundary (multiple of check_termination, or max_iter)

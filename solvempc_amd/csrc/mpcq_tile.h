@@ -177,43 +177,6 @@ __device__ __forceinline__ void tile_mv(const T *__restrict__ im, const T (&x)[X
         for (int r = 0; r < 4; r++) y[4 * t + r] = acc[t][r];
 }
 
-// The same product for G independent 16-QP groups of one wave: every A operand read from LDS feeds
-// G MFMAs, and the G accumulator chains interleave (more independent work per wave).
-template <typename T, int G, int NTO, int KS, int KSP, int XN>
-__device__ __forceinline__ void tile_mv_g(const T *__restrict__ im, const T (&x)[G][XN], T (&y)[G][4 * NTO],
-                                          int lane, const T (*init)[4 * NTO])
-{
-    using A = typename Mf<T>::acc;
-    constexpr int VEC = 16 / sizeof(T);
-    constexpr int NG = (KS + VEC - 1) / VEC;
-    typedef T vec __attribute__((ext_vector_type(VEC)));
-    im = fresh_ptr(im);
-    vec opnd[NTO][NG];
-#pragma unroll
-    for (int t = 0; t < NTO; t++)
-#pragma unroll
-        for (int q = 0; q < NG; q++) opnd[t][q] = *(const vec *)(im + TileLayout::at(KSP, VEC, t, q * VEC, lane));
-    A acc[G][NTO];
-#pragma unroll
-    for (int gi = 0; gi < G; gi++)
-#pragma unroll
-        for (int t = 0; t < NTO; t++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) acc[gi][t][r] = init ? init[gi][4 * t + r] : T(0);
-#pragma unroll
-    for (int s = 0; s < KS; s++)
-#pragma unroll
-        for (int t = 0; t < NTO; t++)
-#pragma unroll
-            for (int gi = 0; gi < G; gi++) acc[gi][t] = Mf<T>::mma(opnd[t][s / VEC][s % VEC], x[gi][s], acc[gi][t]);
-#pragma unroll
-    for (int gi = 0; gi < G; gi++)
-#pragma unroll
-        for (int t = 0; t < NTO; t++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) y[gi][4 * t + r] = acc[gi][t][r];
-}
-
 // The 4 x 4 x 1 MFMA's partial sums of the last, 4-row tile (rem_* below) to the tile layout: lane
 // (g, c) holds p_i = sum over k = g (mod 4) of row i of the tile, for QP c; row i belongs to lane
 // group g = i.  Two lane-swap stages (v_permlane32_swap: lanes 32-63 of the first operand with lanes
@@ -227,6 +190,70 @@ __device__ __forceinline__ float rem_reduce(const Mf<float>::acc &p)
     const float q1 = __uint_as_float(r13[0]) + __uint_as_float(r13[1]);  // rows 1 | 3
     auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(q0), __float_as_uint(q1), false, false);
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);                // row g
+}
+
+// The same product for G independent 16-QP groups of one wave: every A operand read from LDS feeds
+// G MFMAs, and the G accumulator chains interleave (more independent work per wave).
+// REM (f32, the last tile holds 4 real rows): that tile on v_mfma_f32_4x4x1_16b, its A fragment read
+// from the 16x16x4 image's lane (g, 4 (c & 3)) (see reg_mv), then rem_reduce; init added after it.
+template <typename T, int G, int NTO, int KS, int KSP, int XN, bool REM = false>
+__device__ __forceinline__ void tile_mv_g(const T *__restrict__ im, const T (&x)[G][XN], T (&y)[G][4 * NTO],
+                                          int lane, const T (*init)[4 * NTO])
+{
+    using A = typename Mf<T>::acc;
+    constexpr int VEC = 16 / sizeof(T);
+    constexpr int NG = (KS + VEC - 1) / VEC;
+    constexpr int NF = REM ? NTO - 1 : NTO;
+    static_assert(!REM || std::is_same<T, float>::value, "4x4x1 remainder tile: f32 only");
+    typedef T vec __attribute__((ext_vector_type(VEC)));
+    im = fresh_ptr(im);
+    vec opnd[NTO][NG];
+#pragma unroll
+    for (int t = 0; t < NTO; t++) {
+        const int ln = (REM && t == NF) ? ((lane & 48) | ((lane & 3) << 2)) : lane;
+#pragma unroll
+        for (int q = 0; q < NG; q++) opnd[t][q] = *(const vec *)(im + TileLayout::at(KSP, VEC, t, q * VEC, ln));
+    }
+    A acc[G][NTO];
+#pragma unroll
+    for (int gi = 0; gi < G; gi++)
+#pragma unroll
+        for (int t = 0; t < NTO; t++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) acc[gi][t][r] = (init && t < NF) ? init[gi][4 * t + r] : T(0);
+#pragma unroll
+    for (int s = 0; s < KS; s++)
+#pragma unroll
+        for (int t = 0; t < NTO; t++)
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                if constexpr (REM) {
+                    if (t == NF) {
+                        acc[gi][t] = __builtin_amdgcn_mfma_f32_4x4x1f32(opnd[t][s / VEC][s % VEC], x[gi][s], acc[gi][t], 0, 0, 0);
+                        continue;
+                    }
+                }
+                acc[gi][t] = Mf<T>::mma(opnd[t][s / VEC][s % VEC], x[gi][s], acc[gi][t]);
+            }
+#pragma unroll
+    for (int gi = 0; gi < G; gi++)
+#pragma unroll
+        for (int t = 0; t < NTO; t++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                if constexpr (REM) {
+                    if (t == NF) {
+                        if (r == 0) {
+                            const T v = rem_reduce(acc[gi][t]);
+                            y[gi][4 * t] = init ? v + init[gi][4 * t] : v;
+                        } else {
+                            y[gi][4 * t + r] = T(0);
+                        }
+                        continue;
+                    }
+                }
+                y[gi][4 * t + r] = acc[gi][t][r];
+            }
 }
 
 // Products with the A operand held in VGPRs (one f32/f64 register per lane per tile and k-step: the
@@ -320,10 +347,17 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
     constexpr int QPW = 64 * G;                  // QPs per workgroup
     __shared__ __attribute__((aligned(16))) T img[L.total];
     __shared__ T rowv[3 * NCP + 2 * MCP];        // lam, D, Dinv | E, Einv of the plant
+    // q^ of each wave's QPs (lane layout): the dual residual of every check iteration reads it here
+    // instead of re-reading q (fp64, HBM) under the latency of a loaded memory system
+    __shared__ T s_qh[4][G * KN][64];
     T *const s_lam = rowv, *const s_D = rowv + NCP, *const s_Dinv = rowv + 2 * NCP;
     T *const s_E = rowv + 3 * NCP, *const s_Einv = rowv + 3 * NCP + MCP;
-    const int count = a.count_in ? *a.count_in : a.batch;
-    if (blockIdx.x * QPW >= count) return;  // whole workgroup idle in this phase (uniform)
+    // resumed phase: this workgroup serves list segment `seg` (ListSeg), as its workgroup `blk`
+    const bool seglist = a.list_in != nullptr;
+    const int seg = blockIdx.x % ListSeg::kShards;
+    const int count = seglist ? a.count_in[seg * ListSeg::kStride] : a.batch;  // slots of the list it serves
+    const int blk = seglist ? (int)blockIdx.x / ListSeg::kShards : (int)blockIdx.x;
+    if (blk * QPW >= count) return;  // whole workgroup idle in this phase (uniform)
     for (int i = threadIdx.x; i < NCP; i += 256) {
         s_lam[i] = a.ops.lam[i];
         s_D[i] = a.ops.D[i];
@@ -420,12 +454,17 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
     const bool resume = persist ? stage > 0 : a.resume != 0;
     const bool mpc_fe = persist ? (stage == 0 && a.mpc) : a.mpc != 0;  // front end: the QP's first stage
 
-    // ---- per-QP data (element v = 4 s + g of this lane's QP column), per group.  Every global load
-    // of a group is issued (index clamped into the row, not branched) before any of it is used.
-    T qh[G][NS];  // q^ = c D q (osqp_update_lin_cost): prologue only; the checks re-read q (load_qh)
     T uh[G][MS], lh[G][LFREE ? 1 : MS];
     T rs[ALL_INEQ ? 1 : MS];
     int status[G];
+    T gv[G][NS];                         // W' q^
+    T xs[G][NS], z[G][MS], y[G][MS];     // state: x' (W-basis), z, y
+    T rho[G], rinv[G];
+    int it = 0;
+    {
+    // ---- per-QP data (element v = 4 s + g of this lane's QP column), per group.  Every global load
+    // of a group is issued (index clamped into the row, not branched) before any of it is used.
+    T qh[G][NS];  // q^ = c D q (osqp_update_lin_cost): prologue only; the checks re-read q (load_qh)
 #pragma unroll
     for (int gi = 0; gi < G; gi++) {
         const int b = b_[gi];
@@ -483,6 +522,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
         for (int s = 0; s < NS; s++) {
             const int v = 4 * s + g;
             qh[gi][s] = (s < KN && v < n) ? (T)((qk[s < KN ? s : 0] * fe[FE_D + v]) * c64) : T(0);
+            if (s < KN) s_qh[threadIdx.x >> 6][gi * KN + (s < KN ? s : 0)][lane] = qh[gi][s];
         }
         int bad = 0, tchg = 0;
 #pragma unroll
@@ -514,7 +554,6 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
     }
 
     // g = W' q^ (the q-part of the KKT right-hand side in the W-basis)
-    T gv[G][NS];
     tile_mv_g<T, G, NT, KN, KNP>(img + L.Wt, qh, gv, lane, nullptr);
 #pragma unroll
     for (int gi = 0; gi < G; gi++)
@@ -522,9 +561,6 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
         for (int s = 0; s < NS; s++) gv[gi][s] = s < KN ? -gv[gi][s] : T(0);  // xi starts from -g
 
     // ---- state: x' (W-basis), z, y; rho persists across solves (OSQP)
-    T xs[G][NS], z[G][MS], y[G][MS];
-    T rho[G], rinv[G];
-    int it = 0;
     const bool load_state = resume || (a.warm && !a.fresh);
 #pragma unroll
     for (int gi = 0; gi < G; gi++) {
@@ -543,6 +579,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
             y[gi][s] = (load_state && s < KM) ? a.ys[(size_t)b * mcs + 4 * s + g] : T(0);
         }
         rinv[gi] = T(1) / rho[gi];
+    }
     }
     it = __builtin_amdgcn_readfirstlane(it);  // lane 0 is always a live column; a phase shares `it`
     T dk[G][NS];
@@ -627,6 +664,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
         }
     }
 
+    long long info_cycles = 0;
     const int ct = st.check_termination;
     const int ai = (st.adaptive_rho && a.adaptive_interval) ? a.adaptive_interval : 0;
     const int stop = persist ? a.stops[stage] : a.stop_iter;
@@ -764,6 +802,9 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
             }
         }
         it++;
+#ifdef MPCQ_INFO_STAMPS  // debug build: cycles in info iterations -> phase stamp 5
+        const long long t_info = a.stamps ? (long long)__builtin_amdgcn_s_memtime() : 0;
+#endif
         const bool at_check = it == next_check;
         const bool at_adapt = it == next_adapt;
         if (at_check) next_check += ct;
@@ -834,58 +875,91 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
 #pragma unroll
             for (int s = KM; s < MS; s++) dy[gi][s] = T(0);
 
-        // ---- update_info: residuals in the scaled space (reported unscaled), 4-lane reductions
+        // ---- update_info: residuals in the scaled space (reported unscaled), 4-lane reductions.  The
+        // termination test reads the unscaled-space norms (_s: E^-1, D^-1 applied) unless
+        // scaled_termination, adapt_rho the scaled-space ones (_r): each set only where it is read.
+        const bool need_r = scaled_term || at_adapt, need_s = !scaled_term;
         T ax_z[G], ax_zs[G], zn_s[G], zn_r[G], axn_s[G], axn_r[G];
         {
             T ax[G][MS];
-            tile_mv_g<T, G, MT, KN, KNP>(img + L.B, xs, ax, lane, nullptr);
+            if constexpr (PAIRED) {  // A x: the top rows B~ x' (B's first NT tiles), the bottom ones their negation
+                T axt[G][NS];
+                tile_mv_g<T, G, NT, KN, KNP, NS, REM4>(img + L.B, xs, axt, lane, nullptr);
+#pragma unroll
+                for (int gi = 0; gi < G; gi++)
+#pragma unroll
+                    for (int s = 0; s < MS; s++)
+                        ax[gi][s] = s < KN ? axt[gi][s] : (s < KM ? -axt[gi][s < KM ? s - KN : 0] : T(0));
+            } else {
+                tile_mv_g<T, G, MT, KN, KNP>(img + L.B, xs, ax, lane, nullptr);
+            }
             const T *Einv = fresh_ptr((const T *)s_Einv);
 #pragma unroll
             for (int gi = 0; gi < G; gi++) {
                 ax_z[gi] = ax_zs[gi] = zn_s[gi] = zn_r[gi] = axn_s[gi] = axn_r[gi] = T(0);
+                if (need_r) {
 #pragma unroll
-                for (int s = 0; s < KM; s++) {
-                    const T r = ax[gi][s] - z[gi][s];
-                    const T ei = Einv[4 * s + g];
-                    ax_z[gi] = nrm(ax_z[gi], r);
-                    ax_zs[gi] = nrm(ax_zs[gi], ei * r);
-                    zn_r[gi] = nrm(zn_r[gi], z[gi][s]);
-                    zn_s[gi] = nrm(zn_s[gi], ei * z[gi][s]);
-                    axn_r[gi] = nrm(axn_r[gi], ax[gi][s]);
-                    axn_s[gi] = nrm(axn_s[gi], ei * ax[gi][s]);
+                    for (int s = 0; s < KM; s++) {
+                        const T r = ax[gi][s] - z[gi][s];
+                        ax_z[gi] = nrm(ax_z[gi], r);
+                        zn_r[gi] = nrm(zn_r[gi], z[gi][s]);
+                        axn_r[gi] = nrm(axn_r[gi], ax[gi][s]);
+                    }
+                }
+                if (need_s) {
+#pragma unroll
+                    for (int s = 0; s < KM; s++) {
+                        const T r = ax[gi][s] - z[gi][s];
+                        const T ei = Einv[4 * s + g];
+                        ax_zs[gi] = nrm(ax_zs[gi], ei * r);
+                        zn_s[gi] = nrm(zn_s[gi], ei * z[gi][s]);
+                        axn_s[gi] = nrm(axn_s[gi], ei * ax[gi][s]);
+                    }
                 }
             }
         }
         T dr_r[G], dr_s[G], qn_r[G], qn_s[G], atyn_r[G], atyn_s[G], pxn_r[G], pxn_s[G];
         {
             T px[G][NS], aty[G][NS];
-            tile_mv_g<T, G, NT, KN, KNP>(img + L.PW, xs, px, lane, nullptr);
-            tile_mv_g<T, G, NT, KM, KMP>(img + L.AhT, y, aty, lane, nullptr);
+            tile_mv_g<T, G, NT, KN, KNP, NS, REM4>(img + L.PW, xs, px, lane, nullptr);
+            if constexpr (PAIRED) {  // A' y = A~' (y_top - y_bot): the first KN k-steps of the A^' image
+                T yd[G][KNR];
+#pragma unroll
+                for (int gi = 0; gi < G; gi++)
+#pragma unroll
+                    for (int s = 0; s < KN; s++) yd[gi][s] = y[gi][s] - y[gi][s + KN];
+                tile_mv_g<T, G, NT, KN, KMP, KNR, REM4>(img + L.AhT, yd, aty, lane, nullptr);
+            } else {
+                tile_mv_g<T, G, NT, KM, KMP>(img + L.AhT, y, aty, lane, nullptr);
+            }
             const T *Dinv = fresh_ptr((const T *)s_Dinv);
-            const double *qsrc = a.mpc ? a.q_out : a.q;  // this QP's q (written by the prologue in MPC mode)
+            const T(*const qhw)[64] = s_qh[opaque((int)threadIdx.x >> 6)];  // this wave's q^ (prologue)
 #pragma unroll
             for (int gi = 0; gi < G; gi++) {
                 T qh[NS];
-                const int b = opaque(b_[gi]);
 #pragma unroll
-                for (int s = 0; s < KN; s++) {
-                    const int v = 4 * s + g;
-                    qh[s] = v < n ? (T)((qsrc[(size_t)b * n + v] * (double)s_D[v]) * c64) : T(0);
-                }
+                for (int s = 0; s < KN; s++) qh[s] = qhw[gi * KN + s][lane];
                 dr_r[gi] = dr_s[gi] = qn_r[gi] = qn_s[gi] = atyn_r[gi] = atyn_s[gi] = pxn_r[gi] = pxn_s[gi] = T(0);
+                if (need_r) {
 #pragma unroll
-                for (int s = 0; s < KN; s++) {
-                    const T qhs = qh[s];
-                    const T r = (qhs + px[gi][s]) + aty[gi][s];
-                    const T di = Dinv[4 * s + g];
-                    dr_r[gi] = nrm(dr_r[gi], r);
-                    dr_s[gi] = nrm(dr_s[gi], di * r);
-                    qn_r[gi] = nrm(qn_r[gi], qhs);
-                    qn_s[gi] = nrm(qn_s[gi], di * qhs);
-                    atyn_r[gi] = nrm(atyn_r[gi], aty[gi][s]);
-                    atyn_s[gi] = nrm(atyn_s[gi], di * aty[gi][s]);
-                    pxn_r[gi] = nrm(pxn_r[gi], px[gi][s]);
-                    pxn_s[gi] = nrm(pxn_s[gi], di * px[gi][s]);
+                    for (int s = 0; s < KN; s++) {
+                        const T r = (qh[s] + px[gi][s]) + aty[gi][s];
+                        dr_r[gi] = nrm(dr_r[gi], r);
+                        qn_r[gi] = nrm(qn_r[gi], qh[s]);
+                        atyn_r[gi] = nrm(atyn_r[gi], aty[gi][s]);
+                        pxn_r[gi] = nrm(pxn_r[gi], px[gi][s]);
+                    }
+                }
+                if (need_s) {
+#pragma unroll
+                    for (int s = 0; s < KN; s++) {
+                        const T r = (qh[s] + px[gi][s]) + aty[gi][s];
+                        const T di = Dinv[4 * s + g];
+                        dr_s[gi] = nrm(dr_s[gi], di * r);
+                        qn_s[gi] = nrm(qn_s[gi], di * qh[s]);
+                        atyn_s[gi] = nrm(atyn_s[gi], di * aty[gi][s]);
+                        pxn_s[gi] = nrm(pxn_s[gi], di * px[gi][s]);
+                    }
                 }
             }
         }
@@ -893,13 +967,16 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
         const T cinv = op.cs[1];
 #pragma unroll
         for (int gi = 0; gi < G; gi++) {
-            ax_z[gi] = col_max(ax_z[gi]); ax_zs[gi] = col_max(ax_zs[gi]);
-            zn_s[gi] = col_max(zn_s[gi]); zn_r[gi] = col_max(zn_r[gi]);
-            axn_s[gi] = col_max(axn_s[gi]); axn_r[gi] = col_max(axn_r[gi]);
-            dr_r[gi] = col_max(dr_r[gi]); dr_s[gi] = col_max(dr_s[gi]);
-            qn_r[gi] = col_max(qn_r[gi]); qn_s[gi] = col_max(qn_s[gi]);
-            atyn_r[gi] = col_max(atyn_r[gi]); atyn_s[gi] = col_max(atyn_s[gi]);
-            pxn_r[gi] = col_max(pxn_r[gi]); pxn_s[gi] = col_max(pxn_s[gi]);
+            if (need_r) {
+                ax_z[gi] = col_max(ax_z[gi]); zn_r[gi] = col_max(zn_r[gi]); axn_r[gi] = col_max(axn_r[gi]);
+                dr_r[gi] = col_max(dr_r[gi]); qn_r[gi] = col_max(qn_r[gi]); atyn_r[gi] = col_max(atyn_r[gi]);
+                pxn_r[gi] = col_max(pxn_r[gi]);
+            }
+            if (need_s) {
+                ax_zs[gi] = col_max(ax_zs[gi]); zn_s[gi] = col_max(zn_s[gi]); axn_s[gi] = col_max(axn_s[gi]);
+                dr_s[gi] = col_max(dr_s[gi]); qn_s[gi] = col_max(qn_s[gi]); atyn_s[gi] = col_max(atyn_s[gi]);
+                pxn_s[gi] = col_max(pxn_s[gi]);
+            }
             pri_res[gi] = scaled_term ? ax_z[gi] : ax_zs[gi];
             dua_res[gi] = scaled_term ? dr_r[gi] : cinv * dr_s[gi];
         }
@@ -1098,6 +1175,9 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
 #pragma unroll
             for (int gi = 0; gi < G; gi++) done[gi] = term[gi];
         }
+#ifdef MPCQ_INFO_STAMPS
+        if (a.stamps) info_cycles += (long long)__builtin_amdgcn_s_memtime() - t_info;
+#endif
         if (it == stop && !all_done()) {
             if (!persist) MPCQ_TSTAMP(3, (long long)__builtin_amdgcn_s_memtime());
             // stage / phase boundary: save the running QPs and queue them for the next stage / launch.
@@ -1136,12 +1216,13 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
             if (lane == 0)
                 base = persist ? (int)__hip_atomic_fetch_add(a.sched + TileSched::res(stage + 1, shard), total,
                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                               : atomicAdd(a.count_out, (int)total);
+                               : atomicAdd(a.count_out + (blockIdx.x % ListSeg::kShards) * ListSeg::kStride, (int)total);
             base = __shfl(base, 0);
-            int *const qout = persist ? a.qlist + (size_t)(stage + 1) * a.batch + sh_lo : a.list_out;
+            int *const qout = persist ? a.qlist + (size_t)(stage + 1) * a.batch + sh_lo
+                                      : a.list_out + (blockIdx.x % ListSeg::kShards) * a.list_seg;
 #pragma unroll
             for (int gi = 0; gi < G; gi++) {
-                const unsigned long long below = (1ull << lane) - 1ull;
+                const unsigned long long below = (1ull << c) - 1ull;  // the column's g = 0 lane is lane c
                 int pos = base + __popcll(mask[gi] & below);
 #pragma unroll
                 for (int gj = 0; gj < gi; gj++) pos += __popcll(mask[gj]);
@@ -1154,7 +1235,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
             break;
         }
     }
-    if (!persist) MPCQ_TSTAMP(5, (long long)it);
+    if (!persist) MPCQ_TSTAMP(5, info_cycles);  // cycles in info iterations (checks, adapt, stop)
     };  // run_group
 
     // ---- Work queue (one launch per solve).  After each group a wave claims 16 G QPs of its shard:
@@ -1177,7 +1258,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
         unsigned base = 0, cnt = 0;
         if (!persist) {
             // phase schedule: this wave's 16 G QPs are slots wave_slot.. of the launch's list
-            const int wave_slot = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 * G;
+            const int wave_slot = (blk * 4 + (threadIdx.x >> 6)) * 16 * G;
             if (!first || wave_slot >= count) break;
             k = 0;
             base = (unsigned)wave_slot;
@@ -1231,8 +1312,8 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
             for (int gi = 0; gi < G; gi++) {
                 const unsigned slot = 16 * gi + c;
                 valid[gi] = slot < cnt;
-                const int i = (int)(base + slot);
-                b_[gi] = valid[gi] ? (a.list_in ? a.list_in[i] : a.qp0 + i) : 0;
+                const int i = (int)(base + slot) + (seglist ? seg * a.list_seg : 0);  // list entry
+                b_[gi] = valid[gi] ? (seglist ? a.list_in[i] : a.qp0 + i) : 0;
             }
         } else {
             // the entries were reserved before this claim; poll until their producers wrote them
@@ -1300,7 +1381,9 @@ int tile_launch_variant(const AdmmArgs<T> &a, hipStream_t s)
 }
 
 // occ: 0 = default for the shape/type, else a requested variant (benchmark A/B hook):
-// f32 fast path  occ 3 -> 1 group/wave at 3 waves/SIMD;  occ 2 -> 2 groups/wave at 2 waves/SIMD.
+// f32 paired loop: default 1 group/wave at 3 waves/SIMD;  occ 2 -> 2 groups/wave at 2 waves/SIMD;
+// occ 4 -> 4 waves/SIMD (LDS-limited to 3 workgroups per CU: only with a smaller image set; measured
+// with W, W' out of LDS at 128 VGPRs: spills, 0.50 vs 0.44 ms per cfg2 solve).
 template <typename T, int KN, int KM>
 int tile_launch(const AdmmArgs<T> &a, int occ, hipStream_t s)
 {

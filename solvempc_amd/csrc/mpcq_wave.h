@@ -18,6 +18,13 @@
 
 namespace mpcq {
 
+// Ordering of the LDS broadcast buffers.  The workgroup is ONE wave, and the LDS executes one wave's
+// DS instructions in issue order, so a lane's read after another lane's write of the same word (or a
+// write after a read) needs no s_barrier and no lgkmcnt wait: only the compiler must keep program
+// order (the memory clobber).  (With __syncthreads a broadcast cost a write -> wait -> barrier ->
+// read round trip: ~450 cycles of an ~1,800-cycle tail iteration.)
+__device__ __forceinline__ void wave_sync() { asm volatile("" ::: "memory"); }
+
 template <int CTRL> __device__ __forceinline__ unsigned dpp_u(unsigned v)
 {
     return (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false);
@@ -88,7 +95,7 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
     constexpr int VEC = 16 / sizeof(T);
     constexpr int BN = (NCAP + VEC - 1) / VEC * VEC, BM = (MCAP + VEC - 1) / VEC * VEC;
     const int lane = threadIdx.x;
-    __syncthreads();  // the previous QP of this block is done with the broadcast buffers
+    wave_sync();  // the previous QP of this block is done with the broadcast buffers
     const int n = a.n, m = a.m;
     const bool ln = lane < n, lm = lane < m;
     const size_t po = a.shared ? 0 : (size_t)b * a.ops_stride;
@@ -174,7 +181,7 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
 
     // g = W' q^ (lane k: column k of W)
     if (ln) bcx[lane] = qh;
-    __syncthreads();
+    wave_sync();
     T gk = T(0);
     {
         gk = mem_dot<T, NCAP>(ops + L.W + kl, nc, bcx, gk);
@@ -208,9 +215,9 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
 
     auto finalize = [&]() {
         // x = D W x' (lane i: row i of W)
-        __syncthreads();
+        wave_sync();
         if (ln) bcx[lane] = xs;
-        __syncthreads();
+        wave_sync();
         const T xh = mem_dot<T, NCAP>(ops + L.W + (size_t)kl * nc, 1, bcx, T(0));
         const bool has_sol = status == kSolved || status == kSolvedInaccurate || status == kMaxIterReached;
         if (ln) {
@@ -270,10 +277,10 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
             rij = T(1) / rj;
         }
         const T w = lm ? tt_fma(rj, z, -y) : T(0);
-        __syncthreads();  // previous readers of bcx / bcw are done
+        wave_sync();  // previous readers of bcx / bcw are done
         if (ln) bcx[lane] = xs;
         if (lm) bcw[lane] = w;
-        __syncthreads();
+        wave_sync();
         MPCQ_WSTAMP(1);
         T xi = row_dot(Srow, bcx, gk) + row_dot(Btrow, bcw, T(0));  // two independent chains
         const T eta = xi * dk;
@@ -281,10 +288,10 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
         const T dx = xn - xs;
         xs = xn;
         // ---- z~ = B eta ; relaxation ; projection ; dual update
-        __syncthreads();
+        wave_sync();
         MPCQ_WSTAMP(2);
         if (ln) bcx[lane] = eta;
-        __syncthreads();
+        wave_sync();
         MPCQ_WSTAMP(3);
         const T zt = row_dot(Brow, bcx, T(0));
         T dy = T(0);
@@ -301,10 +308,10 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
         if (!info) continue;
 
         // ---- update_info: residual norms (whole-wave reductions)
-        __syncthreads();
+        wave_sync();
         if (ln) bcx[lane] = xs;
         if (lm) bcw[lane] = y;
-        __syncthreads();
+        wave_sync();
         T ax_z = 0, ax_zs = 0, zn_s = 0, zn_r = 0, axn_s = 0, axn_r = 0;
         if (lm) {
             const T ax = row_dot(Brow, bcx, T(0));
@@ -354,9 +361,9 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
             ndy = wmax(ndy);
             lhs = wsum(lhs);
             if (!(ndy > T(kDivisionTol) && lhs < eps * ndy)) return false;
-            __syncthreads();
+            wave_sync();
             if (lm) bcw[lane] = d;
-            __syncthreads();
+            wave_sync();
             T atd = T(0);
             if (ln) atd = mem_dot<T, MCAP>(ops + L.Ah + lane, nc, bcw, atd);
             const T nat = wmax(ln ? __builtin_fabs(scaled_term ? atd : Dinv_p[lane] * atd) : T(0));
@@ -365,9 +372,9 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
         auto dual_infeasible = [&](T eps) -> bool {
             const T qdx = wsum(ln ? -gk * dx : T(0));  // q^' dx^ = (W' q^)' dx'
             if (!(qdx < T(0))) return false;
-            __syncthreads();
+            wave_sync();
             if (ln) bcx[lane] = dx;
-            __syncthreads();
+            wave_sync();
             T t1 = T(0), t2 = T(0), t3 = T(0);
             if (ln) {
                 t1 = mem_dot<T, NCAP>(ops + L.W + (size_t)lane * nc, 1, bcx, t1);
@@ -449,7 +456,8 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
             if (lane == 0) {
                 a.rhos[b] = rho;
                 a.it_state[b] = it;
-                a.list_out[atomicAdd(a.count_out, 1)] = b;
+                const int sg = blockIdx.x % ListSeg::kShards;
+                a.list_out[sg * a.list_seg + atomicAdd(a.count_out + sg * ListSeg::kStride, 1)] = b;
             }
             return;
         }
@@ -459,14 +467,20 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
 template <typename T, int NCAP, int MCAP, bool ALL_INEQ, bool LFREE>
 __global__ __launch_bounds__(64, 2) void admm_wave_kernel(AdmmArgs<T> a, int nc, int mc)
 {
-    static_assert(NCAP <= 64 && MCAP <= 64, "one row per lane");
+    static_assert(NCAP <= 64 && MCAP <= 64, "one row per lane");  // one wave per workgroup (wave_sync)
     constexpr int VEC = 16 / sizeof(T);
     constexpr int BN = (NCAP + VEC - 1) / VEC * VEC, BM = (MCAP + VEC - 1) / VEC * VEC;
     __shared__ __attribute__((aligned(16))) T bcx[BN];  // x'-side broadcast (x', eta, q^, dx)
     __shared__ __attribute__((aligned(16))) T bcw[BM];  // row-side broadcast (w, y, d)
-    const int count = a.count_in ? *a.count_in : a.batch;
-    for (int slot = blockIdx.x; slot < count; slot += gridDim.x)  // uniform: one wave per block
-        wave_solve_one<T, NCAP, MCAP, ALL_INEQ, LFREE>(a, nc, mc, a.list_in ? a.list_in[slot] : a.qp0 + slot, bcx, bcw);
+    if (a.list_in) {  // a resumed phase's ListSeg list: block b serves segment b % kShards (grid % kShards == 0)
+        const int sg = blockIdx.x % ListSeg::kShards, per = gridDim.x / ListSeg::kShards;
+        const int count = a.count_in[sg * ListSeg::kStride];
+        for (int slot = blockIdx.x / ListSeg::kShards; slot < count; slot += per)  // uniform: one wave per block
+            wave_solve_one<T, NCAP, MCAP, ALL_INEQ, LFREE>(a, nc, mc, a.list_in[sg * a.list_seg + slot], bcx, bcw);
+        return;
+    }
+    for (int slot = blockIdx.x; slot < a.batch; slot += gridDim.x)  // uniform: one wave per block
+        wave_solve_one<T, NCAP, MCAP, ALL_INEQ, LFREE>(a, nc, mc, a.qp0 + slot, bcx, bcw);
 }
 
 

@@ -27,9 +27,10 @@ for p in range(nph):
     rt0, rt1 = s[:, 6], s[:, 7]
     span = (rt1.max() - rt0.min()) / 100.0  # us
     skew = (np.percentile(rt0, 99) - rt0.min()) / 100.0
-    print(f"phase {p}: waves {len(s)} looped {looped.sum()}  span {span:.1f} us  entry skew(p99) {skew:.1f} us  "
-          f"iters at exit {np.unique(s[:, 5])[:6]}")
-    print(f"   image+barrier {q(img)}\n   prologue      {q(pro)}\n   loop          {q(loop)}\n   save          {q(save)}")
+    print(f"phase {p}: waves {len(s)} looped {looped.sum()}  span {span:.1f} us  entry skew(p99) {skew:.1f} us")
+    info = np.where(looped, s[:, 5], 0)  # non-zero only in a -DMPCQ_INFO_STAMPS build
+    print(f"   image+barrier {q(img)}\n   prologue      {q(pro)}\n   loop          {q(loop)}\n"
+          f"    of which info iterations {q(info)}\n   save          {q(save)}")
     lat = (rt1 - rt0) / 100.0
     print(f"   wave lifetime us: med {np.median(lat):.1f} max {lat.max():.1f}; exits in last 10% of span: "
           f"{np.mean(rt1 > rt0.min() + 0.9 * span * 100):.2%}")
