@@ -136,6 +136,14 @@ template <typename V> __device__ __forceinline__ void st_sc1(V *p, V v)
 {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// A hand-off store: write-through (st_sc1) when a workgroup of the same launch reads it (work queue),
+// a plain write-back store when only a later launch does (phase chain: the kernel boundary publishes
+// it, and the XCD's L2 merges the 16-32 B pieces of a QP row before they reach HBM).
+template <typename V> __device__ __forceinline__ void st_handoff(V *p, V v, bool through)
+{
+    if (through) st_sc1(p, v);
+    else *p = v;
+}
 
 template <typename P> __device__ __forceinline__ P fresh_ptr(P p)
 {
@@ -331,10 +339,11 @@ __device__ __forceinline__ void reg_mv(const T (&m1)[NTO][KS], const T (&x1)[G][
 // 6 / 7 s_memrealtime (100 MHz) at entry / exit.
 #define MPCQ_TSTAMP(k, v)                                                                                  \
     do {                                                                                                   \
-        if (a.stamps && (threadIdx.x & 63) == 0) a.stamps[(size_t)(blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (k)] = (v); \
+        if (a.stamps && (threadIdx.x & 63) == 0) a.stamps[(size_t)(blockIdx.x * WPB + (threadIdx.x >> 6)) * 8 + (k)] = (v); \
     } while (0)
-template <typename T, int KN, int KM, bool ALL_INEQ, bool LFREE, int G, int OCC, bool PAIRED = false>
-__global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
+// WPB: waves per workgroup (4, or 8 so that an image set serves 8 waves and 4 waves/SIMD fit the LDS).
+template <typename T, int KN, int KM, bool ALL_INEQ, bool LFREE, int G, int OCC, bool PAIRED = false, int WPB = 4>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void admm_tile_kernel(AdmmArgs<T> a)
 {
     MPCQ_TSTAMP(0, (long long)__builtin_amdgcn_s_memtime());
     MPCQ_TSTAMP(6, (long long)__builtin_amdgcn_s_memrealtime());
@@ -344,12 +353,13 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
     constexpr int NT = L.NT, MT = L.MT, KNP = L.KNP, KMP = L.KMP;
     constexpr int NS = 4 * NT, MS = 4 * MT;  // registers per n- / m-vector
     constexpr int NCP = 16 * NT, MCP = 16 * MT;  // padded row counts (== ctx nc, mc)
-    constexpr int QPW = 64 * G;                  // QPs per workgroup
+    constexpr int NTH = 64 * WPB;                // threads per workgroup
+    constexpr int QPW = 16 * G * WPB;            // QPs per workgroup
     __shared__ __attribute__((aligned(16))) T img[L.total];
     __shared__ T rowv[3 * NCP + 2 * MCP];        // lam, D, Dinv | E, Einv of the plant
     // q^ of each wave's QPs (lane layout): the dual residual of every check iteration reads it here
     // instead of re-reading q (fp64, HBM) under the latency of a loaded memory system
-    __shared__ T s_qh[4][G * KN][64];
+    __shared__ T s_qh[WPB][G * KN][64];
     T *const s_lam = rowv, *const s_D = rowv + NCP, *const s_Dinv = rowv + 2 * NCP;
     T *const s_E = rowv + 3 * NCP, *const s_Einv = rowv + 3 * NCP + MCP;
     // resumed phase: this workgroup serves list segment `seg` (ListSeg), as its workgroup `blk`
@@ -358,12 +368,12 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
     const int count = seglist ? a.count_in[seg * ListSeg::kStride] : a.batch;  // slots of the list it serves
     const int blk = seglist ? (int)blockIdx.x / ListSeg::kShards : (int)blockIdx.x;
     if (blk * QPW >= count) return;  // whole workgroup idle in this phase (uniform)
-    for (int i = threadIdx.x; i < NCP; i += 256) {
+    for (int i = threadIdx.x; i < NCP; i += NTH) {
         s_lam[i] = a.ops.lam[i];
         s_D[i] = a.ops.D[i];
         s_Dinv[i] = a.ops.Dinv[i];
     }
-    for (int i = threadIdx.x; i < MCP; i += 256) {
+    for (int i = threadIdx.x; i < MCP; i += NTH) {
         s_E[i] = a.ops.E[i];
         s_Einv[i] = a.ops.Einv[i];
     }
@@ -373,16 +383,16 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
         typedef T vec __attribute__((ext_vector_type(VEC)));
         const vec *src = (const vec *)a.img;
         vec *dst = (vec *)img;
-        constexpr int NV = (int)(L.total / VEC), PER = (NV + 255) / 256;
+        constexpr int NV = (int)(L.total / VEC), PER = (NV + NTH - 1) / NTH;
         vec buf[PER];
 #pragma unroll
         for (int k = 0; k < PER; k++) {
-            const int i = threadIdx.x + 256 * k;
+            const int i = threadIdx.x + NTH * k;
             buf[k] = src[i < NV ? i : 0];
         }
 #pragma unroll
         for (int k = 0; k < PER; k++) {
-            const int i = threadIdx.x + 256 * k;
+            const int i = threadIdx.x + NTH * k;
             if (i < NV) dst[i] = buf[k];
         }
     }
@@ -394,19 +404,19 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
     __shared__ double fe[FE_TOT];
     {
         const int n = a.n, m = a.m, nx = a.mpc ? a.nx : 0;
-        for (int i = threadIdx.x; i < MCP; i += 256) fe[FE_E + i] = i < m ? (double)a.ops.E[i] : 0.0;
-        for (int i = threadIdx.x; i < NCP; i += 256) fe[FE_D + i] = i < n ? (double)a.ops.D[i] : 0.0;
+        for (int i = threadIdx.x; i < MCP; i += NTH) fe[FE_E + i] = i < m ? (double)a.ops.E[i] : 0.0;
+        for (int i = threadIdx.x; i < NCP; i += NTH) fe[FE_D + i] = i < n ? (double)a.ops.D[i] : 0.0;
         if (a.mpc) {
-            for (int i = threadIdx.x; i < 8 * NCP; i += 256) {
+            for (int i = threadIdx.x; i < 8 * NCP; i += NTH) {
                 const int v = i >> 3, t = i & 7;
                 fe[FE_FX + i] = (v < n && t < nx) ? a.Fx[(size_t)v * nx + t] : 0.0;
             }
-            for (int i = threadIdx.x; i < 8 * MCP; i += 256) {
+            for (int i = threadIdx.x; i < 8 * MCP; i += NTH) {
                 const int v = i >> 3, t = i & 7;
                 fe[FE_SB + i] = (v < m && t < nx) ? a.Sbar[(size_t)v * nx + t] : 0.0;
             }
-            for (int i = threadIdx.x; i < NCP; i += 256) fe[FE_FU + i] = i < n ? a.Fu[i] : 0.0;
-            for (int i = threadIdx.x; i < MCP; i += 256) {
+            for (int i = threadIdx.x; i < NCP; i += NTH) fe[FE_FU + i] = i < n ? a.Fu[i] : 0.0;
+            for (int i = threadIdx.x; i < MCP; i += NTH) {
                 fe[FE_KU + i] = i < m ? a.Ku[i] : 0.0;
                 fe[FE_W0 + i] = i < m ? a.W0[i] : 0.0;
             }
@@ -425,6 +435,17 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
     }
     __syncthreads();  // the only barrier: waves are independent from here on
     MPCQ_TSTAMP(1, (long long)__builtin_amdgcn_s_memtime());
+    // debug build MPCQ_PRO_PART=p: stamp 5 holds the cycles between prologue marks p-1 and p
+#ifdef MPCQ_PRO_PART
+    long long t_pro = (long long)__builtin_amdgcn_s_memtime();
+#define MPCQ_PRO_MARK(k)                                                                            \
+    do {                                                                                            \
+        if ((k) == MPCQ_PRO_PART - 1) t_pro = (long long)__builtin_amdgcn_s_memtime();              \
+        if ((k) == MPCQ_PRO_PART) MPCQ_TSTAMP(5, (long long)__builtin_amdgcn_s_memtime() - t_pro); \
+    } while (0)
+#else
+#define MPCQ_PRO_MARK(k) do { } while (0)
+#endif
 
     const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
     constexpr int KNR = PAIRED ? KN : 1, NTR = PAIRED ? NT : 1;
@@ -487,7 +508,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
                     if (t < nx) s0 += fe[FE_FX + 8 * v + t] * Xv[t];
                 const double s1 = fe[FE_FU + v] * Uv;
                 qk[s] = s0 + s1 + fe[FE_FR + v];
-                if (valid[gi] && v < n) st_sc1(a.q_out + (size_t)b * n + v, qk[s]);  // read by later stages
+                if (valid[gi] && v < n) st_handoff(a.q_out + (size_t)b * n + v, qk[s], persist);  // read by later stages
             }
 #pragma unroll
             for (int s = 0; s < KM; s++) {
@@ -497,7 +518,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
                 for (int t = 0; t < 8; t++)
                     if (t < nx) sx += fe[FE_SB + 8 * v + t] * Xv[t];
                 up[s] = fe[FE_W0 + v] + sx + fe[FE_KU + v] * Uv;
-                if (valid[gi] && v < m) st_sc1(a.u_out + (size_t)b * m + v, up[s]);
+                if (valid[gi] && v < m) st_handoff(a.u_out + (size_t)b * m + v, up[s], persist);
             }
         } else {
 #pragma unroll
@@ -552,6 +573,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
         tchg = col_or(tchg);
         status[gi] = bad ? kInvalidBounds : (tchg ? kTypeChanged : kUnsolved);
     }
+    MPCQ_PRO_MARK(1);
 
     // g = W' q^ (the q-part of the KKT right-hand side in the W-basis)
     tile_mv_g<T, G, NT, KN, KNP>(img + L.Wt, qh, gv, lane, nullptr);
@@ -559,6 +581,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
     for (int gi = 0; gi < G; gi++)
 #pragma unroll
         for (int s = 0; s < NS; s++) gv[gi][s] = s < KN ? -gv[gi][s] : T(0);  // xi starts from -g
+    MPCQ_PRO_MARK(2);
 
     // ---- state: x' (W-basis), z, y; rho persists across solves (OSQP)
     const bool load_state = resume || (a.warm && !a.fresh);
@@ -582,6 +605,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
     }
     }
     it = __builtin_amdgcn_readfirstlane(it);  // lane 0 is always a live column; a phase shares `it`
+    MPCQ_PRO_MARK(3);
     T dk[G][NS];
     auto set_dk = [&]() {
         const T *lam = fresh_ptr((const T *)s_lam);
@@ -591,6 +615,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
             for (int s = 0; s < NS; s++) dk[gi][s] = T(1) / (T(1) + rho[gi] * lam[4 * s + g]);  // lam padded 0
     };
     set_dk();
+    MPCQ_PRO_MARK(4);
 
     const T alpha = (T)st.alpha, oma = T(1) - (T)st.alpha;
     const T eps_abs = (T)st.eps_abs, eps_rel = (T)st.eps_rel;
@@ -599,7 +624,9 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
     for (int gi = 0; gi < G; gi++) done[gi] = !valid[gi];
 
     // ---- write the results of the `mine` QPs (OSQP store_solution / update_info; warm-start state)
-    auto finalize = [&](const bool (&mine)[G]) {
+    // Uold: U of each column read ahead of time (the info iteration prefetches it, so that U += x(0)
+    // does not wait on a global load after the termination test), or null: read it here.
+    auto finalize = [&](const bool (&mine)[G], const double *Uold) {
         // x = D W x'  (all lanes run the MFMA; `mine` lanes store)
         T xh[G][NS];
         tile_mv_g<T, G, NT, KN, KNP>(img + L.W, xs, xh, lane, nullptr);
@@ -616,7 +643,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
                 if (s < KN && v < n) {
                     const double xv = has_sol ? (double)xh[gi][s] * (double)s_D[v] : __builtin_nan("");
                     if (a.x) a.x[(size_t)b * n + v] = xv;
-                    if (v == 0 && a.mpc_u && sta == kSolved) a.U[b] = a.U[b] + xv;  // U += x(0)  (:105)
+                    if (v == 0 && a.mpc_u && sta == kSolved) a.U[b] = (Uold ? Uold[gi] : a.U[b]) + xv;  // U += x(0)  (:105)
                 }
             }
 #pragma unroll
@@ -658,12 +685,13 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
             any = any || mine[gi];
         }
         if (wave_any(any)) {
-            finalize(mine);
+            finalize(mine, nullptr);
 #pragma unroll
             for (int gi = 0; gi < G; gi++) done[gi] = done[gi] || mine[gi];
         }
     }
 
+    MPCQ_PRO_MARK(5);
     long long info_cycles = 0;
     const int ct = st.check_termination;
     const int ai = (st.adaptive_rho && a.adaptive_interval) ? a.adaptive_interval : 0;
@@ -803,7 +831,17 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
         }
         it++;
 #ifdef MPCQ_INFO_STAMPS  // debug build: cycles in info iterations -> phase stamp 5
-        const long long t_info = a.stamps ? (long long)__builtin_amdgcn_s_memtime() : 0;
+        long long t_info = a.stamps ? (long long)__builtin_amdgcn_s_memtime() : 0;
+#endif
+        // MPCQ_INFO_PART=p (with MPCQ_INFO_STAMPS): stamp 5 counts only the part between marks p-1, p
+#if defined(MPCQ_INFO_STAMPS) && defined(MPCQ_INFO_PART)
+#define MPCQ_INFO_MARK(k)                                                                          \
+    do {                                                                                           \
+        if (a.stamps && (k) == MPCQ_INFO_PART - 1) t_info = (long long)__builtin_amdgcn_s_memtime(); \
+        if (a.stamps && (k) == MPCQ_INFO_PART) info_cycles += (long long)__builtin_amdgcn_s_memtime() - t_info; \
+    } while (0)
+#else
+#define MPCQ_INFO_MARK(k) do { } while (0)
 #endif
         const bool at_check = it == next_check;
         const bool at_adapt = it == next_adapt;
@@ -870,6 +908,10 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
             continue;
         }
         iterate(std::true_type{});
+        double Uold[G];  // U of the running columns, ahead of a finalize (latency hidden by the checks)
+#pragma unroll
+        for (int gi = 0; gi < G; gi++) Uold[gi] = (a.mpc_u && g == 0 && !done[gi]) ? a.U[opaque(b_[gi])] : 0.0;
+        MPCQ_INFO_MARK(1);
 #pragma unroll
         for (int gi = 0; gi < G; gi++)
 #pragma unroll
@@ -980,6 +1022,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
             pri_res[gi] = scaled_term ? ax_z[gi] : ax_zs[gi];
             dua_res[gi] = scaled_term ? dr_r[gi] : cinv * dr_s[gi];
         }
+        MPCQ_INFO_MARK(2);
 
         // OSQP is_primal_infeasible on delta_y = dy (this iteration's dual step), per group.
         auto primal_infeasible = [&](T eps, const bool (&need)[G], bool (&res)[G]) {
@@ -1130,6 +1173,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
             for (int gi = 0; gi < G; gi++)
                 if (!term[gi] && s0[gi] != kUnsolved) { status[gi] = s0[gi]; term[gi] = true; }
         }
+        MPCQ_INFO_MARK(3);
         if (at_adapt) {  // adapt_rho / compute_rho_estimate (scaled-space norms)
 #pragma unroll
             for (int gi = 0; gi < G; gi++) {
@@ -1164,6 +1208,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
             for (int gi = 0; gi < G; gi++)
                 if (!term[gi]) { status[gi] = s2[gi] != kUnsolved ? s2[gi] : kMaxIterReached; term[gi] = true; }
         }
+        MPCQ_INFO_MARK(4);
         {
             bool newly[G], any = false;
 #pragma unroll
@@ -1171,11 +1216,12 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
                 newly[gi] = term[gi] && !done[gi];
                 any = any || newly[gi];
             }
-            if (wave_any(any)) finalize(newly);
+            if (wave_any(any)) finalize(newly, Uold);
 #pragma unroll
             for (int gi = 0; gi < G; gi++) done[gi] = term[gi];
         }
-#ifdef MPCQ_INFO_STAMPS
+        MPCQ_INFO_MARK(5);
+#if defined(MPCQ_INFO_STAMPS) && !defined(MPCQ_INFO_PART)
         if (a.stamps) info_cycles += (long long)__builtin_amdgcn_s_memtime() - t_info;
 #endif
         if (it == stop && !all_done()) {
@@ -1191,20 +1237,20 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
                 if (run) {
 #pragma unroll
                     for (int s = 0; s < NS; s++)
-                        if (s < KN) st_sc1(a.xs + (size_t)b * ncs + 4 * s + g, xs[gi][s]);
+                        if (s < KN) st_handoff(a.xs + (size_t)b * ncs + 4 * s + g, xs[gi][s], persist);
 #pragma unroll
                     for (int s = 0; s < MS; s++)
                         if (s < KM) {
-                            st_sc1(a.zs + (size_t)b * mcs + 4 * s + g, z[gi][s]);
-                            st_sc1(a.ys + (size_t)b * mcs + 4 * s + g, y[gi][s]);
+                            st_handoff(a.zs + (size_t)b * mcs + 4 * s + g, z[gi][s], persist);
+                            st_handoff(a.ys + (size_t)b * mcs + 4 * s + g, y[gi][s], persist);
                         }
                     if (g == 0) {
-                        st_sc1(a.rhos + b, rho[gi]);
-                        st_sc1(a.it_state + b, it);
+                        st_handoff(a.rhos + b, rho[gi], persist);
+                        st_handoff(a.it_state + b, it, persist);
                     }
                 }
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (persist) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (work queue: before the flags)
             unsigned long long mask[G];
             unsigned total = 0;
 #pragma unroll
@@ -1235,7 +1281,9 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
             break;
         }
     }
+#ifndef MPCQ_PRO_PART
     if (!persist) MPCQ_TSTAMP(5, info_cycles);  // cycles in info iterations (checks, adapt, stop)
+#endif
     };  // run_group
 
     // ---- Work queue (one launch per solve).  After each group a wave claims 16 G QPs of its shard:
@@ -1258,7 +1306,7 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
         unsigned base = 0, cnt = 0;
         if (!persist) {
             // phase schedule: this wave's 16 G QPs are slots wave_slot.. of the launch's list
-            const int wave_slot = (blk * 4 + (threadIdx.x >> 6)) * 16 * G;
+            const int wave_slot = (blk * WPB + (threadIdx.x >> 6)) * 16 * G;
             if (!first || wave_slot >= count) break;
             k = 0;
             base = (unsigned)wave_slot;
@@ -1359,16 +1407,17 @@ __global__ __launch_bounds__(256, OCC) void admm_tile_kernel(AdmmArgs<T> a)
 // Launch one tile-kernel variant: one workgroup per 64 G QPs (phase schedule), or for the work
 // queue at most as many workgroups as are resident at once (the kernel's occupancy x CUs, cached per
 // variant), each looping over claimed groups.
-template <typename T, int KN, int KM, bool AI, bool LF, int G, int OCC, bool PAIRED = false>
+template <typename T, int KN, int KM, bool AI, bool LF, int G, int OCC, bool PAIRED = false, int WPB = 4>
 int tile_launch_variant(const AdmmArgs<T> &a, hipStream_t s)
 {
-    auto kern = admm_tile_kernel<T, KN, KM, AI, LF, G, OCC, PAIRED>;
-    int blocks = (a.batch + 64 * G - 1) / (64 * G);
+    auto kern = admm_tile_kernel<T, KN, KM, AI, LF, G, OCC, PAIRED, WPB>;
+    constexpr int QPW = 16 * G * WPB;
+    int blocks = (a.batch + QPW - 1) / QPW;
     if (a.persistent) {
         static int resident = 0;
         if (!resident) {
             int per_cu = 0, dev = 0, cus = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess ||
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * WPB, 0) != hipSuccess ||
                 hipGetDevice(&dev) != hipSuccess ||
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu < 1)
                 return -2;
@@ -1376,7 +1425,7 @@ int tile_launch_variant(const AdmmArgs<T> &a, hipStream_t s)
         }
         blocks = blocks < resident ? blocks : resident;
     }
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * WPB), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -1394,6 +1443,7 @@ int tile_launch(const AdmmArgs<T> &a, int occ, hipStream_t s)
             } else {
                 if (occ == 2) return tile_launch_variant<T, KN, KM, true, true, 2, 2, true>(a, s);
                 if (occ == 4) return tile_launch_variant<T, KN, KM, true, true, 1, 4, true>(a, s);
+                if (occ == 8) return tile_launch_variant<T, KN, KM, true, true, 1, 4, true, 8>(a, s);
                 return tile_launch_variant<T, KN, KM, true, true, 1, 3, true>(a, s);
             }
         }

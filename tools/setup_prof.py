@@ -16,6 +16,7 @@ Ad, Bd = workload.randomized_plants(plant, 2, 0, B)
 ops = mpc.condense({"Ad": Ad, "Bd": Bd, "Cd": np.tile(plant["Cd"], (B, 1)), "K": np.tile(plant["K"], (B, 1)),
                     "Q": np.full(B, plant["Q"]), "R": np.full(B, plant["R"]), "RD": np.full(B, plant["RD"])}, N)
 out = os.path.abspath("gpurun_out/setup_prof.bin")
+os.makedirs(os.path.dirname(out), exist_ok=True)
 os.environ["MPCQ_SETUP_PROF"] = out
 s = sm.BatchSolver(N, 2 * N, B, n_plants=B)
 s.setup(ops["P"], np.zeros((B, N)), ops["A"], np.full((B, 2 * N), -1.7e308), np.full((B, 2 * N), 255.0))
