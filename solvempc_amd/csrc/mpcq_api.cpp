@@ -57,6 +57,7 @@ struct mpcq_ctx {
     unsigned *d_sched = nullptr;  // tile work queue: TileSched counters
     int *d_qlist = nullptr;       //                  [stage][batch] queue entries
     bool wq_last = false;         // the last solve ran the work queue (its error word is valid)
+    bool count0_clean = false;    // phase 0's ListSeg counters are zero (the last phase chain's final launch zeroed them)
     long long *d_stamps = nullptr;  // debug (MPCQ_TILE_STAMPS)
     hipStream_t last = nullptr;
     int nx = 0;
@@ -612,7 +613,12 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
     const int np = phase_stops(c->set, stops);
     const int seg = mpcq::ListSeg::cap(B);
     const size_t lcap = (size_t)mpcq::ListSeg::kShards * seg;
-    if (hipMemsetAsync(c->d_counts, 0, 4 * (size_t)np * mpcq::ListSeg::kCounters, s) != hipSuccess) return -2;
+    // Counter blocks: launch p zeroes block p + 1 (its successor's output) and a chain's final launch,
+    // when it is at least the third, zeroes block 0 for the next solve; only a chain that could not
+    // leave block 0 clean costs a memset here.
+    if (!c->count0_clean && hipMemsetAsync(c->d_counts, 0, 4 * (size_t)mpcq::ListSeg::kCounters, s) != hipSuccess)
+        return -2;
+    c->count0_clean = false;
     const int mpc = a.mpc;
     const char *te = std::getenv("MPCQ_TAIL_PHASE");
     const int tail_from = wave_only ? 0 : (te ? std::atoi(te) : 3);
@@ -636,6 +642,9 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
         a.stop_iter = stops[p];
         a.resume = p > 0;
         a.mpc = p == 0 ? mpc : 0;  // later phases read q, u from the buffers phase 0 filled
+        const bool final_launch = p + 1 == np || (p >= tail_from && c->dims.n <= 32 && c->dims.m <= 64);
+        a.zero_cnt = final_launch ? nullptr : c->d_counts + (size_t)(p + 1) * mpcq::ListSeg::kCounters;
+        a.zero_cnt0 = (final_launch && p >= 2) ? c->d_counts : nullptr;
         int rc;
         if (p >= tail_from && c->dims.n <= 32 && c->dims.m <= 64) {
             // one QP per wave carries no idle columns: the rest of the solve is one launch (a resumed
@@ -643,6 +652,7 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
             a.stop_iter = c->set.max_iter;
             rc = wave_launch<T>(c, a, p == 0 ? B : 2048, s);
             if (rc) return rc;
+            c->count0_clean = a.zero_cnt0 != nullptr;
             np_run = p + (stp && *stp ? 1 : 0);  // (the stamps dump includes the wave launch)
             break;
         }
@@ -651,6 +661,7 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
                  ? mpcq_internal_tile_launch_f32((const mpcq::AdmmArgs<float> *)&a, c->KN, c->KM, s)
                  : mpcq_internal_tile_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->KN, c->KM, s);
         if (rc) return rc;
+        c->count0_clean = a.zero_cnt0 != nullptr;
         np_run = p + 1;
     }
     if (stp && *stp) {

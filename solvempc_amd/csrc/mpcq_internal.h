@@ -174,6 +174,9 @@ struct AdmmArgs {
     const int *list_in;         // active QP indices of this phase (null: identity 0..batch-1), ListSeg layout
     const int *count_in;        // ListSeg counters of list_in (null: batch)
     int *list_out, *count_out;  // QPs still running at stop_iter (appended, ListSeg layout)
+    // ListSeg counter blocks this launch zeroes on entry (workgroup 0; null: none): the next phase's
+    // output counters, and in a chain's last launch the first phase's (for the next solve)
+    int *zero_cnt, *zero_cnt0;
     int list_seg;               // ListSeg segment capacity
     int *it_state;              // [batch] iterations done so far in this solve
     int qp0;                    // QP index of identity-list slot 0 (sub-batch parts of a tile solve)

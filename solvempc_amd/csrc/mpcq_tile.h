@@ -367,6 +367,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     const int seg = blockIdx.x % ListSeg::kShards;
     const int count = seglist ? a.count_in[seg * ListSeg::kStride] : a.batch;  // slots of the list it serves
     const int blk = seglist ? (int)blockIdx.x / ListSeg::kShards : (int)blockIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < ListSeg::kShards) {  // counters no launch of this chain is using
+        if (a.zero_cnt) a.zero_cnt[threadIdx.x * ListSeg::kStride] = 0;
+        if (a.zero_cnt0) a.zero_cnt0[threadIdx.x * ListSeg::kStride] = 0;
+    }
     if (blk * QPW >= count) return;  // whole workgroup idle in this phase (uniform)
     for (int i = threadIdx.x; i < NCP; i += NTH) {
         s_lam[i] = a.ops.lam[i];
@@ -463,8 +467,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     const unsigned B = (unsigned)a.batch;
     const unsigned nsh = gridDim.x < (unsigned)TileSched::kShards ? gridDim.x : (unsigned)TileSched::kShards;
     const unsigned shard = blockIdx.x % nsh;
-    const unsigned sh_lo = (unsigned)((unsigned long long)B * shard / nsh);
-    const unsigned sh_hi = (unsigned)((unsigned long long)B * (shard + 1) / nsh);
+    unsigned sh_lo = 0, sh_hi = 0;  // (the divisions only where they are used)
+    if (persist) {
+        sh_lo = (unsigned)((unsigned long long)B * shard / nsh);
+        sh_hi = (unsigned)((unsigned long long)B * (shard + 1) / nsh);
+    }
 
     // One group of 16 G QPs (column c of group gi: QP b_[gi], live if valid[gi]) from the start of
     // `stage` to its stop iteration (work queue), or of this launch's phase (phase schedule).
@@ -475,6 +482,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     const bool resume = persist ? stage > 0 : a.resume != 0;
     const bool mpc_fe = persist ? (stage == 0 && a.mpc) : a.mpc != 0;  // front end: the QP's first stage
 
+    MPCQ_PRO_MARK(10);
     T uh[G][MS], lh[G][LFREE ? 1 : MS];
     T rs[ALL_INEQ ? 1 : MS];
     int status[G];
@@ -510,6 +518,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 qk[s] = s0 + s1 + fe[FE_FR + v];
                 if (valid[gi] && v < n) st_handoff(a.q_out + (size_t)b * n + v, qk[s], persist);  // read by later stages
             }
+            MPCQ_PRO_MARK(11);
 #pragma unroll
             for (int s = 0; s < KM; s++) {
                 const int v = 4 * s + g;
@@ -520,6 +529,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 up[s] = fe[FE_W0 + v] + sx + fe[FE_KU + v] * Uv;
                 if (valid[gi] && v < m) st_handoff(a.u_out + (size_t)b * m + v, up[s], persist);
             }
+            MPCQ_PRO_MARK(12);
         } else {
 #pragma unroll
             for (int s = 0; s < KN; s++) {
@@ -545,6 +555,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             qh[gi][s] = (s < KN && v < n) ? (T)((qk[s < KN ? s : 0] * fe[FE_D + v]) * c64) : T(0);
             if (s < KN) s_qh[threadIdx.x >> 6][gi * KN + (s < KN ? s : 0)][lane] = qh[gi][s];
         }
+        MPCQ_PRO_MARK(13);
         int bad = 0, tchg = 0;
 #pragma unroll
         for (int s = 0; s < MS; s++) {
@@ -574,6 +585,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
         status[gi] = bad ? kInvalidBounds : (tchg ? kTypeChanged : kUnsolved);
     }
     MPCQ_PRO_MARK(1);
+    MPCQ_PRO_MARK(14);
 
     // g = W' q^ (the q-part of the KKT right-hand side in the W-basis)
     tile_mv_g<T, G, NT, KN, KNP>(img + L.Wt, qh, gv, lane, nullptr);

@@ -472,6 +472,10 @@ __global__ __launch_bounds__(64, 2) void admm_wave_kernel(AdmmArgs<T> a, int nc,
     constexpr int BN = (NCAP + VEC - 1) / VEC * VEC, BM = (MCAP + VEC - 1) / VEC * VEC;
     __shared__ __attribute__((aligned(16))) T bcx[BN];  // x'-side broadcast (x', eta, q^, dx)
     __shared__ __attribute__((aligned(16))) T bcw[BM];  // row-side broadcast (w, y, d)
+    if (blockIdx.x == 0 && threadIdx.x < ListSeg::kShards) {  // counters no launch of this chain is using
+        if (a.zero_cnt) a.zero_cnt[threadIdx.x * ListSeg::kStride] = 0;
+        if (a.zero_cnt0) a.zero_cnt0[threadIdx.x * ListSeg::kStride] = 0;
+    }
     if (a.list_in) {  // a resumed phase's ListSeg list: block b serves segment b % kShards (grid % kShards == 0)
         const int sg = blockIdx.x % ListSeg::kShards, per = gridDim.x / ListSeg::kShards;
         const int count = a.count_in[sg * ListSeg::kStride];
