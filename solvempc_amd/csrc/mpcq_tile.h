@@ -29,6 +29,9 @@
 #ifndef MPCQ_REM4
 #define MPCQ_REM4 1  // build switch for A/B: 0 runs the remainder tile as a full 16x16x4 tile
 #endif
+#ifndef MPCQ_PK
+#define MPCQ_PK 1  // build switch for A/B: 0 runs the f32 plain iterations on scalar VALU ops
+#endif
 
 namespace mpcq {
 
@@ -811,6 +814,132 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 }
         }
     };
+    // piter_fast's f32 arithmetic on packed pairs (v_pk_fma/add/mul_f32: two elements per VALU issue,
+    // the f32 vector and matrix work share the SIMD's issue time): element pairs (2k, 2k + 1) of each
+    // half-vector (top rows s < KN, bottom rows KN + s) with an odd last element on its own.  The state
+    // is held in pairs for the plain iterations between two info iterations; every operation and its
+    // order are piter_fast's, so the results are bit-identical to it.
+    constexpr bool PK = PAIRED && std::is_same<T, float>::value && MPCQ_PK;
+    auto piter_pk_loop = [&](const T (&rS)[NTR][KNR], const T (&rBt)[NTR][KNR], const T (&rB)[NTR][KNR],
+                             T (&sx)[G][NS], const T (&adk)[G][KNR], const int nxt) {
+        if constexpr (PK) {
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            constexpr int NPR = KN / 2;
+            constexpr bool ODD = (KN & 1) != 0;
+            auto pfma = [](f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); };
+            f2 XP[G][NPR], ZT[G][NPR], ZB[G][NPR], YT[G][NPR], YB[G][NPR], AD[G][NPR], RH[G];
+            float X1[G], ZT1[G], ZB1[G], YT1[G], YB1[G], AD1[G];
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                RH[gi] = f2{rho[gi], rho[gi]};
+#pragma unroll
+                for (int k = 0; k < NPR; k++) {
+                    XP[gi][k] = f2{xs[gi][2 * k], xs[gi][2 * k + 1]};
+                    ZT[gi][k] = f2{z[gi][2 * k], z[gi][2 * k + 1]};
+                    ZB[gi][k] = f2{z[gi][KN + 2 * k], z[gi][KN + 2 * k + 1]};
+                    YT[gi][k] = f2{y[gi][2 * k], y[gi][2 * k + 1]};
+                    YB[gi][k] = f2{y[gi][KN + 2 * k], y[gi][KN + 2 * k + 1]};
+                    AD[gi][k] = f2{adk[gi][2 * k], adk[gi][2 * k + 1]};
+                }
+                if constexpr (ODD) {
+                    X1[gi] = xs[gi][KN - 1];
+                    ZT1[gi] = z[gi][KN - 1];
+                    ZB1[gi] = z[gi][2 * KN - 1];
+                    YT1[gi] = y[gi][KN - 1];
+                    YB1[gi] = y[gi][2 * KN - 1];
+                    AD1[gi] = adk[gi][KN - 1];
+                }
+            }
+            const f2 OMA = f2{oma, oma};
+            do {
+                it++;
+                T wt[G][KNR];  // w~ = rho ((z - yt)_top - (z - yt)_bot)
+#pragma unroll
+                for (int gi = 0; gi < G; gi++) {
+#pragma unroll
+                    for (int k = 0; k < NPR; k++) {
+                        const f2 w = RH[gi] * ((ZT[gi][k] - YT[gi][k]) - (ZB[gi][k] - YB[gi][k]));
+                        wt[gi][2 * k] = w.x;
+                        wt[gi][2 * k + 1] = w.y;
+                    }
+                    if constexpr (ODD) wt[gi][KN - 1] = rho[gi] * ((ZT1[gi] - YT1[gi]) - (ZB1[gi] - YB1[gi]));
+                }
+                T xi[G][NS];
+                reg_mv<T, G, NT, KN, KNR, false, KNR, REM4>(rBt, wt, rBt, wt, xi, sx);  // xi = (-g + S x') + B~' w~
+                T xv[G][NS];  // x' as the next S x' product's operand
+#pragma unroll
+                for (int gi = 0; gi < G; gi++) {
+#pragma unroll
+                    for (int k = 0; k < NPR; k++) {
+                        const f2 e = AD[gi][k] * f2{xi[gi][2 * k], xi[gi][2 * k + 1]};  // eta' = alpha eta
+                        xi[gi][2 * k] = e.x;
+                        xi[gi][2 * k + 1] = e.y;
+                        XP[gi][k] = pfma(OMA, XP[gi][k], e);                           // x' = eta' + (1 - alpha) x'
+                        xv[gi][2 * k] = XP[gi][k].x;
+                        xv[gi][2 * k + 1] = XP[gi][k].y;
+                    }
+                    if constexpr (ODD) {
+                        xi[gi][KN - 1] = AD1[gi] * xi[gi][KN - 1];
+                        X1[gi] = tt_fma(oma, X1[gi], xi[gi][KN - 1]);
+                        xv[gi][KN - 1] = X1[gi];
+                    }
+#pragma unroll
+                    for (int s = KN; s < NS; s++) xv[gi][s] = T(0);
+                }
+                T zt[G][NS];
+                reg_mv<T, G, NT, KN, NS, false, KNR, REM4>(rB, xi, rB, wt, zt, nullptr);  // alpha z~_top = B~ eta'
+                reg_mv<T, G, NT, KN, NS, false, KNR, REM4>(rS, xv, rS, wt, sx, gv);       // next: -g + S x'
+#pragma unroll
+                for (int gi = 0; gi < G; gi++) {
+#pragma unroll
+                    for (int k = 0; k < NPR; k++) {
+                        const f2 zp = f2{zt[gi][2 * k], zt[gi][2 * k + 1]};
+                        f2 t = pfma(OMA, ZT[gi][k], zp) + YT[gi][k];  // t = (1 - alpha) z + zt' + yt
+                        f2 zn = f2{vmin(t.x, uh[gi][2 * k]), vmin(t.y, uh[gi][2 * k + 1])};
+                        YT[gi][k] = t - zn;
+                        ZT[gi][k] = zn;
+                        t = pfma(OMA, ZB[gi][k], -zp) + YB[gi][k];
+                        zn = f2{vmin(t.x, uh[gi][KN + 2 * k]), vmin(t.y, uh[gi][KN + 2 * k + 1])};
+                        YB[gi][k] = t - zn;
+                        ZB[gi][k] = zn;
+                    }
+                    if constexpr (ODD) {
+                        float t = tt_fma(oma, ZT1[gi], zt[gi][KN - 1]) + YT1[gi];
+                        float zn = vmin(t, uh[gi][KN - 1]);
+                        YT1[gi] = t - zn;
+                        ZT1[gi] = zn;
+                        t = tt_fma(oma, ZB1[gi], -zt[gi][KN - 1]) + YB1[gi];
+                        zn = vmin(t, uh[gi][2 * KN - 1]);
+                        YB1[gi] = t - zn;
+                        ZB1[gi] = zn;
+                    }
+                }
+            } while (it + 1 < nxt);
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+#pragma unroll
+                for (int k = 0; k < NPR; k++) {
+                    xs[gi][2 * k] = XP[gi][k].x;
+                    xs[gi][2 * k + 1] = XP[gi][k].y;
+                    z[gi][2 * k] = ZT[gi][k].x;
+                    z[gi][2 * k + 1] = ZT[gi][k].y;
+                    z[gi][KN + 2 * k] = ZB[gi][k].x;
+                    z[gi][KN + 2 * k + 1] = ZB[gi][k].y;
+                    y[gi][2 * k] = YT[gi][k].x;
+                    y[gi][2 * k + 1] = YT[gi][k].y;
+                    y[gi][KN + 2 * k] = YB[gi][k].x;
+                    y[gi][KN + 2 * k + 1] = YB[gi][k].y;
+                }
+                if constexpr (ODD) {
+                    xs[gi][KN - 1] = X1[gi];
+                    z[gi][KN - 1] = ZT1[gi];
+                    z[gi][2 * KN - 1] = ZB1[gi];
+                    y[gi][KN - 1] = YT1[gi];
+                    y[gi][2 * KN - 1] = YB1[gi];
+                }
+            }
+        }
+    };
     if (!persist) MPCQ_TSTAMP(2, (long long)__builtin_amdgcn_s_memtime());
     while (!all_done()) {
         if constexpr (PAIRED) {
@@ -831,10 +960,14 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
 #pragma unroll
                     for (int s = 0; s < KM; s++) y[gi][s] = y[gi][s] * rinv[gi];  // y -> yt = y / rho
                 }
-                do {
-                    it++;
-                    piter_fast(rS, rBt, rB, sx, adk);
-                } while (it + 1 < nxt);
+                if constexpr (PK) {
+                    piter_pk_loop(rS, rBt, rB, sx, adk, nxt);
+                } else {
+                    do {
+                        it++;
+                        piter_fast(rS, rBt, rB, sx, adk);
+                    } while (it + 1 < nxt);
+                }
 #pragma unroll
                 for (int gi = 0; gi < G; gi++)
 #pragma unroll
