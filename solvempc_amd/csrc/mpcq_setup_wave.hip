@@ -34,9 +34,9 @@ struct SetupWaveShape {
         s.Ph = o; o += (size_t)n * s.ld;
         s.Ah = o; o += (size_t)m * s.ld;
         s.L = o;  o += (size_t)n * s.ld;
-        s.T = o;  o += (size_t)n * s.ld;
+        s.T = o;  o += (size_t)s.ne * s.ld;
         s.C = o;  o += (size_t)s.ne * s.ld;
-        s.V = o;  o += (size_t)s.ne * s.ld;
+        s.V = s.T;  // V reuses T's space: T (L^-1 G) is dead once C = T' is formed
         s.Dv = o; o += n;
         s.Ev = o; o += m;
         s.Dt = o; o += n;
@@ -224,6 +224,10 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
     for (int e = t; e < ne * ne; e += 64) {
         const int i = e / ne, k = e % ne;
         C[i * ld + k] = (i < n && k < n) ? Tm[k * ld + i] : 0.0;
+    }
+    __syncthreads();
+    for (int e = t; e < ne * ne; e += 64) {  // (V aliases Tm)
+        const int i = e / ne, k = e % ne;
         V[i * ld + k] = (i == k) ? 1.0 : 0.0;
     }
     __syncthreads();

@@ -274,20 +274,26 @@ __device__ __forceinline__ void tile_mv_g(const T *__restrict__ im, const T (&x)
 // v_mfma_f32_4x4x1_16b (16 blocks of 4 rows x 4 QPs, one k each: a quarter of a 16x16x4's issue
 // cycles) with the A fragment lane (g, c) = A[16 (NTO - 1) + (c & 3)][4 s + g] and the iterate
 // register as B operand, then rem_reduce; its init is added after the reduction.
-template <typename T, int G, int NTO, int KS, int XN, bool TWO, int XN2, bool REM = false>
+// RMODE (REM only) defers the remainder tile's lane reduction across two products: 1 = leave its
+// 4x4x1 partial sums unreduced in rem[] and put init's remainder element (not the product's) into y;
+// 2 = start the remainder chain from rem[] (the partials of a mode-1 product), reduce, add init.
+template <typename T, int G, int NTO, int KS, int XN, bool TWO, int XN2, bool REM = false, int RMODE = 0>
 __device__ __forceinline__ void reg_mv(const T (&m1)[NTO][KS], const T (&x1)[G][XN], const T (&m2)[NTO][KS],
-                                       const T (&x2)[G][XN2], T (&y)[G][4 * NTO], const T (*init)[4 * NTO])
+                                       const T (&x2)[G][XN2], T (&y)[G][4 * NTO], const T (*init)[4 * NTO],
+                                       typename Mf<T>::acc *rem = nullptr)
 {
     using A = typename Mf<T>::acc;
     constexpr int NF = REM ? NTO - 1 : NTO;  // full 16-row tiles
     static_assert(!REM || std::is_same<T, float>::value, "4x4x1 remainder tile: f32 only");
+    static_assert(RMODE == 0 || REM, "deferred remainder reduction: remainder tile only");
     A acc[G][NTO];
 #pragma unroll
     for (int gi = 0; gi < G; gi++)
 #pragma unroll
         for (int t = 0; t < NTO; t++)
 #pragma unroll
-            for (int r = 0; r < 4; r++) acc[gi][t][r] = (init && t < NF) ? init[gi][4 * t + r] : T(0);
+            for (int r = 0; r < 4; r++)
+                acc[gi][t][r] = (init && t < NF) ? init[gi][4 * t + r] : ((RMODE == 2 && t == NF) ? rem[gi][r] : T(0));
     auto step = [&](const T (&m)[NTO][KS], auto &x, int s) {
 #pragma unroll
         for (int t = 0; t < NTO; t++)
@@ -314,6 +320,13 @@ __device__ __forceinline__ void reg_mv(const T (&m1)[NTO][KS], const T (&x1)[G][
         for (int t = 0; t < NTO; t++)
 #pragma unroll
             for (int r = 0; r < 4; r++) {
+                if constexpr (REM && RMODE == 1) {
+                    if (t == NF) {
+                        if (r == 0) rem[gi] = acc[gi][t];
+                        y[gi][4 * t + r] = (init && r == 0) ? init[gi][4 * t] : T(0);
+                        continue;
+                    }
+                }
                 if constexpr (REM) {
                     if (t == NF) {
                         if (r == 0) {
@@ -817,11 +830,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     // piter_fast's f32 arithmetic on packed pairs (v_pk_fma/add/mul_f32: two elements per VALU issue,
     // the f32 vector and matrix work share the SIMD's issue time): element pairs (2k, 2k + 1) of each
     // half-vector (top rows s < KN, bottom rows KN + s) with an odd last element on its own.  The state
-    // is held in pairs for the plain iterations between two info iterations; every operation and its
-    // order are piter_fast's, so the results are bit-identical to it.
+    // is held in pairs for the plain iterations between two info iterations.  With the 4x4x1 remainder
+    // tile (REM4) the partial sums of S x' rows 16.. are not reduced on their own but seed the next xi's
+    // remainder chain (one lane reduction per iteration fewer; the sum is reassociated there), otherwise
+    // every operation and its order are piter_fast's.
     constexpr bool PK = PAIRED && std::is_same<T, float>::value && MPCQ_PK;
     auto piter_pk_loop = [&](const T (&rS)[NTR][KNR], const T (&rBt)[NTR][KNR], const T (&rB)[NTR][KNR],
-                             T (&sx)[G][NS], const T (&adk)[G][KNR], const int nxt) {
+                             T (&sx)[G][NS], const T (&adk)[G][KNR], typename Mf<T>::acc (&srem)[G], const int nxt) {
         if constexpr (PK) {
             typedef float f2 __attribute__((ext_vector_type(2)));
             constexpr int NPR = KN / 2;
@@ -865,7 +880,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                     if constexpr (ODD) wt[gi][KN - 1] = rho[gi] * ((ZT1[gi] - YT1[gi]) - (ZB1[gi] - YB1[gi]));
                 }
                 T xi[G][NS];
-                reg_mv<T, G, NT, KN, KNR, false, KNR, REM4>(rBt, wt, rBt, wt, xi, sx);  // xi = (-g + S x') + B~' w~
+                if constexpr (REM4) reg_mv<T, G, NT, KN, KNR, false, KNR, REM4, 2>(rBt, wt, rBt, wt, xi, sx, srem);
+                else reg_mv<T, G, NT, KN, KNR, false, KNR, REM4>(rBt, wt, rBt, wt, xi, sx);  // xi = (-g + S x') + B~' w~
                 T xv[G][NS];  // x' as the next S x' product's operand
 #pragma unroll
                 for (int gi = 0; gi < G; gi++) {
@@ -888,7 +904,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 }
                 T zt[G][NS];
                 reg_mv<T, G, NT, KN, NS, false, KNR, REM4>(rB, xi, rB, wt, zt, nullptr);  // alpha z~_top = B~ eta'
-                reg_mv<T, G, NT, KN, NS, false, KNR, REM4>(rS, xv, rS, wt, sx, gv);       // next: -g + S x'
+                if constexpr (REM4) reg_mv<T, G, NT, KN, NS, false, KNR, REM4, 1>(rS, xv, rS, wt, sx, gv, srem);
+                else reg_mv<T, G, NT, KN, NS, false, KNR, REM4>(rS, xv, rS, wt, sx, gv);  // next: -g + S x'
 #pragma unroll
                 for (int gi = 0; gi < G; gi++) {
 #pragma unroll
@@ -952,7 +969,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 T rS[NTR][KNR], rBt[NTR][KNR], rB[NTR][KNR];
                 load_regs(rS, rBt, rB);
                 T sx[G][NS], adk[G][KNR];
-                reg_mv<T, G, NT, KN, NS, false, NS, REM4>(rS, xs, rS, xs, sx, gv);
+                typename Mf<T>::acc srem[G];  // PK: the remainder partials of S x' (reduced inside the next xi)
+                if constexpr (PK && REM4) reg_mv<T, G, NT, KN, NS, false, NS, REM4, 1>(rS, xs, rS, xs, sx, gv, srem);
+                else reg_mv<T, G, NT, KN, NS, false, NS, REM4>(rS, xs, rS, xs, sx, gv);
 #pragma unroll
                 for (int gi = 0; gi < G; gi++) {
 #pragma unroll
@@ -961,7 +980,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                     for (int s = 0; s < KM; s++) y[gi][s] = y[gi][s] * rinv[gi];  // y -> yt = y / rho
                 }
                 if constexpr (PK) {
-                    piter_pk_loop(rS, rBt, rB, sx, adk, nxt);
+                    piter_pk_loop(rS, rBt, rB, sx, adk, srem, nxt);
                 } else {
                     do {
                         it++;
