@@ -399,6 +399,8 @@ int setup_on_device(mpcq_ctx *c, hipStream_t s)
     a.scaling = c->set.scaling;
     a.sigma = c->set.sigma;
     a.rho = c->set.rho;
+    // an fp32 solve reads W to ~1e-7: a basis orthogonal to ~1e-10 saves the last Jacobi sweep
+    a.jacobi_tol = c->dims.dtype == MPCQ_F32 ? 1e-20 : 1e-32;
     a.P = c->d_P;
     a.q0 = c->d_q0;
     a.A = c->d_A;

@@ -100,6 +100,7 @@ struct SetupArgs {
     int n, m, nc, mc, n_plants;
     int scaling;       // Ruiz passes
     double sigma, rho;
+    double jacobi_tol;  // Jacobi stops at off(C)^2 <= jacobi_tol * diag(C)^2 (fp64 solves 1e-32, fp32 1e-20)
     const double *P, *q0, *A, *l0, *u0;  // [plant] n*n, n, m*n, m, m
     double *ops;       // [plant] OpsLayout(nc, mc).total
     int *ctype;        // [plant] mc

@@ -195,7 +195,7 @@ __global__ __launch_bounds__(64) void setup_kernel(SetupArgs a)
                     double v = C[i * n + k] * C[i * n + k];
                     if (i == k) dia += v; else off += v;
                 }
-            sh[2] = (off <= 1e-32 * dia || off < 1e-300) ? 1.0 : 0.0;
+            sh[2] = (off <= a.jacobi_tol * dia || off < 1e-300) ? 1.0 : 0.0;
         }
         __syncthreads();
         if (sh[2] != 0.0) { converged = true; break; }

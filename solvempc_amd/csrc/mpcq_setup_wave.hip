@@ -54,11 +54,32 @@ __device__ inline double limit_scaling_w(double d)
     return d > kMaxScaling ? kMaxScaling : d;
 }
 
+// Whole-wave sum with every lane ending on the same bits (symmetric pairwise adds): DPP quad swaps and
+// row mirrors, then the 16/32-lane swaps (VALU only; a __shfl_xor ladder is 12 LDS-path permutes).
+template <int CTRL> __device__ inline double dpp_f64(double v)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)u, (int)(unsigned)u, CTRL, 0xF, 0xF, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)(u >> 32), (int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ inline double swap_sum_f64(double v, bool w32)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+    auto r = w32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false) : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    auto h = w32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false) : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    auto mk = [](unsigned l, unsigned hh) { return __longlong_as_double((long long)(((unsigned long long)hh << 32) | l)); };
+    return mk(r[0], h[0]) + mk(r[1], h[1]);
+}
 __device__ inline double wave_sum(double v)
 {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    v = v + dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+    v = v + dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+    v = v + dpp_f64<0x141>(v);  // row_half_mirror
+    v = v + dpp_f64<0x140>(v);  // row_mirror
+    v = swap_sum_f64(v, false);
+    return swap_sum_f64(v, true);
 }
 
 // Pair u of round r of the circle ordering on ne (even) indices.
@@ -273,7 +294,7 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
         off = wave_sum(off);
         dia = wave_sum(dia);
         if (a.prof && t == 0) a.prof[(size_t)pl * 16 + 15] = sweep;
-        if (off <= 1e-32 * dia || off < 1e-300) { converged = true; break; }
+        if (off <= a.jacobi_tol * dia || off < 1e-300) { converged = true; break; }
         for (int r = 0; r < ne - 1; r++) {
             if (t < np) {
                 int pp, qq;
