@@ -125,13 +125,17 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
     __syncthreads();
 
     MPCQ_STAMP(1);
-    // ---- Ruiz equilibration + cost normalisation (OSQP scale_data)
+    // ---- Ruiz equilibration + cost normalisation (OSQP scale_data).  A pass's cost factor ct is not
+    // swept over P^ on its own: it stays pending (cp) and is applied inside the next pass's column
+    // norms (max |cp P| = cp max |P|: rounding is monotone) and D-scaling, or by one sweep after the
+    // last pass, so every P^ element is rounded exactly as in the eager order.
+    double cp = 1.0;
     for (int it = 0; it < a.scaling; it++) {
         if (t < n) {
-            double v = 0.0;
-            for (int i = 0; i < n; i++) v = fmax(v, fabs(Ph[i * ld + t]));
-            for (int i = 0; i < m; i++) v = fmax(v, fabs(Ah[i * ld + t]));
-            Dt[t] = 1.0 / sqrt(limit_scaling_w(v));
+            double vp = 0.0, va = 0.0;
+            for (int i = 0; i < n; i++) vp = fmax(vp, fabs(Ph[i * ld + t]));
+            for (int i = 0; i < m; i++) va = fmax(va, fabs(Ah[i * ld + t]));
+            Dt[t] = 1.0 / sqrt(limit_scaling_w(fmax(cp * vp, va)));
         }
         for (int i = t; i < m; i += 64) {
             double v = 0.0;
@@ -141,7 +145,7 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
         __syncthreads();
         for (int e = t; e < n * n; e += 64) {
             const int i = e / n, k = e % n;
-            Ph[i * ld + k] = (Dt[i] * Ph[i * ld + k]) * Dt[k];
+            Ph[i * ld + k] = (Dt[i] * (Ph[i * ld + k] * cp)) * Dt[k];
         }
         for (int e = t; e < m * n; e += 64) {
             const int i = e / n, k = e % n;
@@ -167,9 +171,11 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
             sh[0] *= ct;
         }
         __syncthreads();
-        const double ct = sh[1];
-        for (int e = t; e < n * n; e += 64) Ph[(e / n) * ld + e % n] *= ct;
-        if (t < n) qh[t] *= ct;
+        cp = sh[1];  // (sh[1] is next written three barriers on)
+        if (t < n) qh[t] *= cp;
+    }
+    if (a.scaling > 0) {
+        for (int e = t; e < n * n; e += 64) Ph[(e / n) * ld + e % n] *= cp;
         __syncthreads();
     }
     const double cost = sh[0];
