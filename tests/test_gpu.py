@@ -567,3 +567,30 @@ def test_tile_work_queue_schedule(plant, monkeypatch):
         assert np.array_equal(st1, st3), dtype
         if dtype == "f64":
             assert np.array_equal(it1, it3) and np.abs(x1 - x3).max() <= 1e-9
+
+
+@pytest.mark.gpu
+def test_phase_chain_counters_across_solves(plant, monkeypatch):
+    """One context, consecutive cold solves whose phase chains differ in length (default, one launch,
+    two launches, default again): the list counters the launches keep clean themselves (no per-solve
+    memset) must hand every QP on, so each solve gives the first one's statuses (f64: iterations and
+    |dx| <= 1e-9; the one-launch schedule finishes the tail in the tile kernel, other summation
+    order) and the two default solves are bit-identical."""
+    N, B = 20, 16384
+    ops, X, U, q, u = _problem(plant, N, B, seed=29)
+    s = _gpu_solve(ops, q, u, N, dtype="f64")
+    x0, st0, it0, _ = (s.solution(), *s.info())
+    assert np.all(st0 == sm.SOLVED)
+    for phases in ("0", "3,5", None):
+        if phases is None:
+            monkeypatch.delenv("MPCQ_PHASES", raising=False)
+        else:
+            monkeypatch.setenv("MPCQ_PHASES", phases)
+        s.reset_state()
+        s.solve()
+        x1, st1, it1, _ = (s.solution(), *s.info())
+        assert np.array_equal(st1, st0), phases
+        assert np.array_equal(it1, it0), phases
+        assert np.abs(x1 - x0).max() <= 1e-9, phases
+        if phases is None:
+            assert np.array_equal(x1, x0)
