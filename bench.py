@@ -8,12 +8,18 @@ q and u built on the device from (X, U), OSQP-v0.6 ADMM solve, U += x[0].  Input
 HBM before timing.  Multi-GPU: one process per GPU, each rank solves its own 65,536 QPs (weak
 scaling, shards of one counter-based global stream) and the applied moves are gathered to rank 0
 over RCCL (the path's only exchange).  Prints ONE JSON line on rank 0.
+
+`python bench.py --gpus N` starts its own N ranks (one process per GPU, spawned before anything
+touches a GPU) unless a launcher (torch.distributed.run) already set RANK / WORLD_SIZE.
+`--backend gloo --dry-run` runs the launcher and the gather on the CPU without a device (tests).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -28,7 +34,7 @@ sys.path.insert(0, str(ROOT))
 PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3}
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
@@ -38,7 +44,7 @@ def parse():
     p.add_argument("--dtype", choices=("f64", "f32"), default="f32", help="ADMM iterate type (BASELINE cfg 2: fp32)")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
-    p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--cpu-threads", type=int, default=0, help="threads of the multi-threaded CPU leg (0: all usable)")
     p.add_argument("--workload", choices=("cfg2", "stream", "perplant", "quadrotor"), default="cfg2",
                    help="cfg2: BASELINE config 2 (the headline); stream: config 5 (4,096 plants x --ctrl-steps "
                         "warm-started control steps with a simulated plant, hipGraph-replayed); perplant: config 3 "
@@ -47,13 +53,19 @@ def parse():
                         "condense + setup + one controllerStep each, fp64)")
     p.add_argument("--ctrl-steps", type=int, default=1000, help="control steps per bench step (stream)")
     p.add_argument("--noise", type=float, default=1e-2, help="plant noise std (stream; SURVEY §8d: var 1e-4)")
-    a = p.parse_args()
+    p.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                   help="torch.distributed backend of the gather (nccl = RCCL on ROCm)")
+    p.add_argument("--dry-run", action="store_true",
+                   help="no device: launcher, rendezvous and the gather only (CPU tests of the N > 1 plumbing)")
+    a = p.parse_args(argv)
     if a.workload == "stream" and a.batch == 65536:
         a.batch = 4096
     if a.workload == "perplant" and a.batch == 65536:
         a.batch = 131072  # 1,048,576 / 8 GPUs
         if a.seed == 1:
             a.seed = 2  # SURVEY §8d config 3 seed
+    if a.workload == "stream" and a.seed == 1:
+        a.seed = 4  # SURVEY §8d config 5 seed
     if a.workload == "quadrotor":
         if a.batch == 65536:
             a.batch = 262144  # BASELINE config 4
@@ -65,65 +77,94 @@ def parse():
     return a
 
 
-def cpu_baseline(ops, N, X, U, budget_s, threads):
-    """The oracle (fp64 C restatement of OSQP-0.6, OpenMP) on a bounded sample of the same workload."""
-    import oracle
+# ----------------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
-    l = np.full(2 * N, -np.finfo(np.float64).max)
-    q0, u0 = np.zeros(N), oracle.upper_bound(ops, np.zeros(4), 0.0)
-    q, u = oracle.gradient(ops, X, U), oracle.upper_bound(ops, X, U)
-    nthr = threads or min(16, os.cpu_count() or 1)
-    n = 256
+
+def launch_ranks(a, argv) -> int:
+    """One process per GPU, started before anything in this process touches a GPU.  Each child gets
+    torch.distributed.run's environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT);
+    rank 0's JSON line is relayed.  Returns the worst child exit code."""
+    port = _free_port()
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + argv, env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
+    out, _ = procs[0].communicate()
+    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    sys.stdout.write(out)
+    sys.stdout.flush()
+    return max(rcs, key=abs)
+
+
+def world_from_env(a):
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return rank, world, local
+
+
+# ----------------------------------------------------------------------------- CPU baseline
+def cpu_info() -> dict:
+    model = ""
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return {"model": model, "nproc": os.cpu_count(), "affinity": usable,
+            # the GPU box grants one GPU's job a CPU share (OMP_NUM_THREADS there); all usable cores otherwise
+            "threads": min(usable, omp) if omp > 0 else usable}
+
+
+def _timed(fn, n0: int, total: int, budget: float):
+    """Run fn(n) on growing prefixes until one run takes >= budget/4 s or the whole sample ran."""
+    n = min(n0, total)
     while True:
         t0 = time.perf_counter()
-        oracle.batch_solve(ops["P"], ops["A"], q0, l, u0, q[:n], u[:n], nthreads=nthr)
+        res = fn(n)
         dt = time.perf_counter() - t0
-        if dt > budget_s / 4 or n >= len(X):
-            break
-        n = min(len(X), int(n * max(2.0, budget_s / 4 / max(dt, 1e-3))))
-    return {"value": n / dt, "unit": "QP/s", "cores": nthr, "kind": "port",
-            "sample": f"{n} QPs of the same batch (first {n} states), oracle/osqp_dense.c fp64, "
-                      f"OpenMP {nthr} threads, {dt:.2f} s"}
+        if dt > budget / 4 or n >= total:
+            return n, dt, res
+        n = min(total, int(n * max(2.0, budget / 4 / max(dt, 1e-3))))
 
 
-def cpu_baseline_plants(plant, Ad, Bd, N, X, U, budget_s, threads):
-    """The oracle's per-plant path (condense + setup + one controllerStep, fp64 C, OpenMP) on a
-    bounded sample of the config-3 plants."""
-    import oracle
-
-    nthr = threads or min(16, os.cpu_count() or 1)
-    n = 256
-    while True:
-        t0 = time.perf_counter()
-        oracle.plants_step(plant, Ad[:n], Bd[:n], X[:n], U[:n], N, nthreads=nthr)
-        dt = time.perf_counter() - t0
-        if dt > budget_s / 4 or n >= len(X):
-            break
-        n = min(len(X), int(n * max(2.0, budget_s / 4 / max(dt, 1e-3))))
-    return {"value": n / dt, "unit": "QP/s", "cores": nthr, "kind": "port",
-            "sample": f"{n} plants of the same batch (first {n}): oracle/mpc_batch.c condense + osqp_dense.c "
-                      f"setup + solve, fp64, OpenMP {nthr} threads, {dt:.2f} s"}
+def _parity(du0_gpu, it_gpu, x_ref, it_ref, st_ref) -> dict:
+    """The device's applied moves against the oracle's on the CPU sample (the checker's role)."""
+    ok = st_ref == 1
+    scale = np.maximum(1.0, np.abs(x_ref).max(axis=1))
+    d = np.abs(du0_gpu - np.where(ok, x_ref[:, 0], 0.0))
+    return {"qps": int(len(du0_gpu)), "schedule_match": float(np.mean(it_gpu == it_ref)),
+            "max_abs_du0": float(d.max()), "max_rel_du0": float((d / scale).max())}
 
 
-def cpu_baseline_quadrotor(shared, Ad, Bd, X, U, N, budget_s, threads):
-    """The oracle's MIMO per-plant path (condense + OSQP-0.6 setup + one controllerStep, fp64 C,
-    OpenMP) on a bounded sample of the config-4 plants."""
-    import oracle
-
-    nthr = threads or min(16, os.cpu_count() or 1)
-    n = 64
-    while True:
-        t0 = time.perf_counter()
-        oracle.mimo_plants_step(shared, Ad[:n], Bd[:n], X[:n], U[:n], N, nthreads=nthr)
-        dt = time.perf_counter() - t0
-        if dt > budget_s / 4 or n >= len(X):
-            break
-        n = min(len(X), int(n * max(2.0, budget_s / 4 / max(dt, 1e-3))))
-    return {"value": n / dt, "unit": "QP/s", "cores": nthr, "kind": "port",
-            "sample": f"{n} plants of the same batch (first {n}): oracle/mpc_mimo.c condense + osqp_dense.c "
-                      f"setup + solve, fp64, OpenMP {nthr} threads, {dt:.2f} s"}
+def cpu_baseline(kind: str, run, n0: int, total: int, budget: float, threads: int, what: str):
+    """Time the oracle (`run(n, nthreads)`) single-threaded and on `threads` OpenMP threads over a
+    bounded prefix of the same batch; returns the record and the multi-threaded run's results."""
+    info = cpu_info()
+    thr = threads or info["threads"]
+    n1, dt1, _ = _timed(lambda n: run(n, 1), max(8, n0 // 16), total, budget / 2)
+    n, dt, res = _timed(lambda n: run(n, thr), n0, total, budget / 2)
+    rec = {"value": n / dt, "unit": "QP/s", "cores": thr, "kind": kind,
+           "single_thread": {"value": n1 / dt1, "sample": f"{n1} QPs, {dt1:.2f} s"},
+           "cpu": info,
+           "sample": f"{n} of the batch's QPs (its first {n}): {what}, fp64, OpenMP {thr} threads, {dt:.2f} s"}
+    return rec, n, res
 
 
+# ----------------------------------------------------------------------------- config 4
 def main_quadrotor(a, rank, world, local, dist, dev):
     """BASELINE config 4: every QP its own quad-rotor plant (hover linearisation with +-10% mass and
     inertia, ZOH dt 0.02); one step = device condensing + setup of every plant + one controllerStep
@@ -165,26 +206,9 @@ def main_quadrotor(a, rank, world, local, dist, dev):
         solver.mimo_step_device(X_d.data_ptr(), U_d.data_ptr(), 0, sptr)
         if i is not None:
             ev[i][1].record(stream)
-        mdist.gather_moves(dist, U_d, world, rank, gathered)
+        return mdist.gather_moves(dist, U_d, world, rank, gathered)
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([wall], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+    wall, got = _timed_loop(a, step, dist, world, dev)
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
     setup_ms = float(np.mean([s.elapsed_time(m_) for (s, _), m_ in zip(ev, ev_mid)]))
     solve_ms = float(np.mean([m_.elapsed_time(e) for (_, e), m_ in zip(ev, ev_mid)]))
@@ -196,27 +220,16 @@ def main_quadrotor(a, rank, world, local, dist, dev):
     solve_flops = float(workload.flops_mimo_solve(n, nu, iters, fact).sum())
     dense = float(workload.flops_mimo_dense(N, nx, nu, ny, iters).sum())
     if rank != 0:
-        if dist:
-            dist.destroy_process_group()
-        return
+        return None
     tf = lambda f, ms: f / (ms * 1e-3) / 1e12  # noqa: E731
     peak = PEAK_TFLOPS["f64"]
-    rec = {
-        "metric": "QP solves/sec (quad-rotor n_x=12, n_u=4, N=30 batch)",
-        "value": B * world * a.steps / wall,
-        "unit": "QP/s",
-        "n_gpus": world,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": wall / a.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f64",
-        "data": "synthetic (hover linearisations, mass/inertia +-10% counter-based per plant; X ~ N(0, diag), U ~ U(-w0/2, w0/2))",
-        "config": {"workload": f"cfg4: {B} quad-rotor plants per GPU (n_x {nx}, n_u {nu}, n_y {ny}), N={N} "
+    rec = _header(a, world, B * world * a.steps / wall, wall, "f64",
+                  "QP solves/sec (quad-rotor n_x=12, n_u=4, N=30 batch)",
+                  "synthetic (hover linearisations, mass/inertia +-10% counter-based per plant; X ~ N(0, diag), U ~ U(-w0/2, w0/2))",
+                  {"workload": f"cfg4: {B} quad-rotor plants per GPU (n_x {nx}, n_u {nu}, n_y {ny}), N={N} "
                                f"(n={n}, m={2 * n}): on-device MIMO condensing + setup + one controllerStep each",
-                   "batch_per_gpu": B, "horizon": N, "parallelism": f"dp{world}"},
+                   "batch_per_gpu": B, "horizon": N, "parallelism": f"dp{world}"})
+    rec.update({
         # dominant stage: the per-QP solve (Gauss-Jordan KKT inverse + ADMM iterations, fp64 VALU)
         "roofline": {"bound": "valu", "achieved": tf(solve_flops, solve_ms), "peak": peak, "unit": "TFLOP/s",
                      "frac": tf(solve_flops, solve_ms) / peak, "traffic": None,
@@ -234,12 +247,60 @@ def main_quadrotor(a, rank, world, local, dist, dev):
                              "note": "SURVEY §8d count: dense condensing + Ruiz + one KKT LDL + iters x F_iter(n, m)"},
         "iters": {"mean": float(iters.mean()), "max": int(iters.max()),
                   "solved_frac": float(np.mean(status == sm.SOLVED)), "rho_adapted_frac": float(np.mean(fact > 1))},
-    }
+        "collective": _collective(dist, world, got),
+    })
     if a.cpu_seconds > 0:
-        rec["cpu_baseline"] = cpu_baseline_quadrotor(sh, Ad, Bd, X, U, N, a.cpu_seconds, a.cpu_threads)
-    print(json.dumps(rec))
-    if dist:
-        dist.destroy_process_group()
+        import oracle
+
+        run = lambda n, t: oracle.mimo_plants_step(sh, Ad[:n], Bd[:n], X[:n], U[:n], N, nthreads=t)  # noqa: E731
+        rec["cpu_baseline"], ns, (U_ref, x_ref, st_ref, it_ref) = cpu_baseline(
+            "port", run, 64, B, a.cpu_seconds, a.cpu_threads,
+            "oracle/mpc_mimo.c condense + osqp_dense.c setup + one controllerStep per plant")
+        du = U_d[:ns].cpu().numpy() - U[:ns]
+        rec["parity"] = _parity(du[:, 0], iters[:ns], x_ref, it_ref, st_ref)
+    return rec
+
+
+# ----------------------------------------------------------------------------- shared pieces
+def _header(a, world, value, wall, dtype, metric, data, config):
+    return {"metric": metric, "value": value, "unit": "QP/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": wall / a.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": data, "config": config}
+
+
+def _collective(dist, world, got):
+    """What the gather saw: the process group's world size and how many moves reached rank 0."""
+    if world == 1:
+        return {"backend": None, "world_size": 1, "gathered": int(got[0].numel())}
+    return {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+            "gathered": int(sum(t.numel() for t in got))}
+
+
+def _timed_loop(a, step, dist, world, dev):
+    """W untimed warmup steps, then K timed steps between barrier + synchronize; max over ranks."""
+    import torch
+
+    sync = (lambda: torch.cuda.synchronize()) if dev.type == "cuda" else (lambda: None)  # noqa: E731
+    for _ in range(a.warmup):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    got = None
+    for i in range(a.steps):
+        got = step(i)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([wall], device=dev if a.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    return wall, got
 
 
 def traffic_per_solve(dtype, batch, N):
@@ -254,11 +315,41 @@ def traffic_per_solve(dtype, batch, N):
     return d.get("bytes_per_solve")
 
 
-def main():
-    a = parse()
-    from solvempc_amd import dist as mdist
+def main_dry(a, rank, world, dist):
+    """--dry-run: the launcher, the rendezvous and the per-step gather of the applied moves on the
+    CPU (gloo), no device work.  value is null: nothing is solved."""
+    import torch
 
-    rank, world, local = mdist.world_from_env(a.gpus)
+    from solvempc_amd import dist as mdist
+    from solvempc_amd import workload
+
+    start, count = mdist.weak_block(a.batch, rank)
+    _, U = workload.mpc_states(a.seed, start, count)
+    U_t = torch.from_numpy(U)
+    gathered = [torch.empty_like(U_t) for _ in range(world)] if rank == 0 else None
+    wall, got = _timed_loop(a, lambda i=None: mdist.gather_moves(dist, U_t, world, rank, gathered), dist, world,
+                            torch.device("cpu"))
+    if rank != 0:
+        return None
+    rec = _header(a, world, None, wall, a.dtype, "QP solves/sec (n_x=4, n_u=1, N=20 batch)",
+                  "dry run: no device, no solve", {"workload": "dry run of the launcher and the gather",
+                                                    "batch_per_gpu": a.batch, "parallelism": f"dp{world}"})
+    rec["dry_run"] = True
+    rec["collective"] = _collective(dist, world, got)
+    full = torch.cat(got).numpy()
+    rec["collective"]["matches_stream"] = bool(np.array_equal(full, workload.mpc_states(a.seed, 0, a.batch * world)[1]))
+    return rec
+
+
+# ----------------------------------------------------------------------------- main
+def main():
+    argv = sys.argv[1:]
+    a = parse(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a, argv))
+    rank, world, local = world_from_env(a)
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}")
     import torch
 
     dist = None
@@ -266,15 +357,31 @@ def main():
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if a.backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(a.backend, rank=rank, world_size=world)
+    elif not a.dry_run:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world)
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if a.workload == "quadrotor":
-        return main_quadrotor(a, rank, world, local, dist, dev)
+    try:
+        if a.dry_run:
+            rec = main_dry(a, rank, world, dist)
+        elif a.workload == "quadrotor":
+            rec = main_quadrotor(a, rank, world, local, dist, torch.device("cuda", local))
+        else:
+            rec = main_lti(a, rank, world, local, dist, torch.device("cuda", local))
+        if rank == 0:
+            print(json.dumps(rec))
+    finally:
+        if dist:
+            dist.destroy_process_group()
+
+
+def main_lti(a, rank, world, local, dist, dev):
+    """Configs 2 (shared plant), 3 (per-plant condensing + setup + step) and 5 (stream)."""
+    import torch
 
     import solvempc_amd as sm
+    from solvempc_amd import dist as mdist
     from solvempc_amd import workload
 
     N, B = a.horizon, a.batch
@@ -284,11 +391,12 @@ def main():
                           N, device=local)
     ops = {k: v[0] for k, v in ops.items()}
     start, count = mdist.weak_block(B, rank)  # weak scaling: every rank owns B QPs of the global stream
-    X, U = workload.mpc_states(a.seed, start, count)
+    stream_mode = a.workload == "stream"
+    perplant = a.workload == "perplant"
+    X, U = workload.stream_states(a.seed, start, count) if stream_mode else workload.mpc_states(a.seed, start, count)
     l = np.full(2 * N, -np.finfo(np.float64).max)
     u0 = ops["W0"].copy()  # W0 + Sbar 0 + Ku 0 (:43)
 
-    perplant = a.workload == "perplant"
     if perplant:  # config 3: every QP its own plant, condensed and set up on the device each step
         Ad, Bd = workload.randomized_plants(plant, a.seed, start, count)
         solver = sm.BatchSolver(N, 2 * N, B, B, a.dtype, local)
@@ -306,151 +414,130 @@ def main():
     sptr = stream.cuda_stream
     gathered = [torch.empty_like(U_d) for _ in range(world)] if rank == 0 else None
 
-    stream_mode = a.workload == "stream"
     if stream_mode:
         solver.mpc_set_plant(plant["Ad"], plant["Bd"])
         side = torch.cuda.Stream(dev)  # graph capture needs a non-default stream
         stream, sptr = side, side.cuda_stream
         X0_d = X_d.clone()
-    ctrl_base = [0]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    ev_mid = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
+    cur = torch.cuda.current_stream(dev)
 
-    def launch(i=None):
-        if stream_mode:  # config 5: ctrl_steps warm-started control steps + plant updates (hipGraph)
-            solver.mpc_run_device(X_d.data_ptr(), U_d.data_ptr(), plant["xref"], a.ctrl_steps, a.seed, start,
-                                  ctrl_base[0], a.noise, sptr)
-            ctrl_base[0] += a.ctrl_steps
-        else:
-            if perplant:  # condensing + Ruiz + eigen-basis setup of every plant, on the device
-                solver.mpc_setup_plants_device(4, 10, *[t.data_ptr() for t in plant_d], sptr)
-                if i is not None:
-                    ev_mid[i].record(stream)  # setup | solve boundary (same stream)
-            solver.mpc_step_device(X_d.data_ptr(), U_d.data_ptr(), plant["xref"], sptr)
-
-    def reset():
+    def step(i=None):
         U_d.copy_(U0_d)          # every step: the reference's first control step of each plant
         if not perplant:         # (perplant: the setup inside the step resets the state)
             solver.reset_state()  # post-setup solver state (x = z = y = 0, rho = settings.rho)
         if stream_mode:
             X_d.copy_(X0_d)
-            ctrl_base[0] = 0
-
-    cur = torch.cuda.current_stream(dev)
-
-    def step(i=None):
-        reset()
-        if stream_mode:
             stream.wait_stream(cur)  # the resets above ran on the current stream
         if i is not None:
             ev[i][0].record(stream)
-        launch(i)
+        if stream_mode:  # config 5: ctrl_steps warm-started control steps + plant updates (hipGraph)
+            solver.mpc_run_device(X_d.data_ptr(), U_d.data_ptr(), plant["xref"], a.ctrl_steps, a.seed, start, 0,
+                                  a.noise, sptr)
+        else:
+            if perplant:  # condensing + Ruiz + KKT setup of every plant, on the device
+                solver.mpc_setup_plants_device(4, 10, *[t.data_ptr() for t in plant_d], sptr)
+                if i is not None:
+                    ev_mid[i].record(stream)  # setup | solve boundary (same stream)
+            solver.mpc_step_device(X_d.data_ptr(), U_d.data_ptr(), plant["xref"], sptr)
         if i is not None:
             ev[i][1].record(stream)
         if stream_mode:
             cur.wait_stream(stream)
-        mdist.gather_moves(dist, U_d, world, rank, gathered)
+        return mdist.gather_moves(dist, U_d, world, rank, gathered)
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
-    ev_mid = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([wall], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+    wall, got = _timed_loop(a, step, dist, world, dev)
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
     if perplant:
         setup_ms = float(np.mean([s.elapsed_time(m_) for (s, _), m_ in zip(ev, ev_mid)]))
         solve_ms = float(np.mean([m_.elapsed_time(e) for (_, e), m_ in zip(ev, ev_mid)]))
 
     status, iters, _ = solver.info()
-    qps_per_step = B * (a.ctrl_steps if stream_mode else 1)
-    # stream: iterations of the last control step stand for every step (estimate, see "flops_note")
     kind, paired = solver.path()
-    reps = a.ctrl_steps if stream_mode else 1
-    flops = float(workload.flops_per_qp(N, 2 * N, 4, iters, paired=paired).sum()) * reps
-    flops_dense = float(workload.flops_per_qp(N, 2 * N, 4, iters).sum()) * reps
+    qps_per_step = B * (a.ctrl_steps if stream_mode else 1)
+    if stream_mode:  # iterations every QP ran over all control steps of the last bench step (device counters)
+        it_total = solver.stream_iterations()
+        flops = float(workload.flops_per_qp_total(N, 2 * N, 4, it_total, a.ctrl_steps, paired=paired).sum())
+        flops_dense = float(workload.flops_per_qp_total(N, 2 * N, 4, it_total, a.ctrl_steps).sum())
+    else:
+        flops = float(workload.flops_per_qp(N, 2 * N, 4, iters, paired=paired).sum())
+        flops_dense = float(workload.flops_per_qp(N, 2 * N, 4, iters).sum())
     achieved = flops / (kern_ms * 1e-3) / 1e12
-    if perplant:
-        setup_flops = B * workload.flops_plant_setup(N, 2 * N)
     solved = float(np.mean(status == sm.SOLVED))
-
     if rank != 0:
-        if dist:
-            dist.destroy_process_group()
-        return
+        return None
     total_qps = qps_per_step * world * a.steps / wall
-    rec = {
-        "metric": "QP solves/sec (n_x=4, n_u=1, N=20 batch)",
-        "value": total_qps,
-        "unit": "QP/s",
-        "n_gpus": world,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": wall / a.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": a.dtype,
-        "data": "synthetic (counter-based X ~ N(0, diag(.1,.1,.05,.5)), U ~ U(-1,1); reference plant config)",
-        "config": ({"workload": f"cfg2: {B} identical LTI plants per GPU, N={N} (n={N}, m={2 * N}), "
-                                f"one controllerStep each", "batch_per_gpu": B, "horizon": N,
-                    "parallelism": f"dp{world}"} if a.workload == "cfg2" else
-                   {"workload": f"cfg3: {B} randomised plants per GPU (Ad, Bd +-2% ~ N(0,1), rho(Ad) < 1), N={N}: "
-                                f"on-device condensing + setup + one controllerStep each",
-                    "batch_per_gpu": B, "horizon": N, "parallelism": f"dp{world}"} if perplant else
-                   {"workload": f"cfg5: {B} plants per GPU x {a.ctrl_steps} warm-started control steps, "
-                                f"simulated plant (noise std {a.noise}), hipGraph-replayed, N={N}",
-                    "batch_per_gpu": B, "horizon": N, "ctrl_steps": a.ctrl_steps, "parallelism": f"dp{world}"}),
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS[a.dtype], "unit": "TFLOP/s",
-                     "frac": achieved / PEAK_TFLOPS[a.dtype], "traffic": traffic_per_solve(a.dtype, B, N),
-                     "kernel": f"admm_{kind}_kernel{' (paired loop)' if paired else ''} (all phase launches of one solve)",
-                     "kernel_ms": kern_ms, "flops_per_step": flops,
-                     "dense_equivalent": {"flops_per_step": flops_dense,
-                                          "achieved": flops_dense / (kern_ms * 1e-3) / 1e12,
-                                          "frac": flops_dense / (kern_ms * 1e-3) / 1e12 / PEAK_TFLOPS[a.dtype]},
-                     "flops_note": "algorithmic: sum over QPs of iters*F_iter + checks*F_check + front end "
-                                   "(SURVEY §8d, DESIGN §4.1), actual per-QP iteration counts"
-                                   + ("; F_iter counts the m/2-row products the paired loop performs "
-                                      "(dense_equivalent: the dense 4nm count)" if paired else "")
-                                   + ("; stream: last control step's counts x ctrl_steps (estimate)" if stream_mode else "")},
-        "iters": {"mean": float(iters.mean()), "max": int(iters.max()), "solved_frac": solved},
-    }
+    config = ({"workload": f"cfg2: {B} identical LTI plants per GPU, N={N} (n={N}, m={2 * N}), one controllerStep each",
+               "batch_per_gpu": B, "horizon": N, "parallelism": f"dp{world}"} if a.workload == "cfg2" else
+              {"workload": f"cfg3: {B} randomised plants per GPU (Ad, Bd +-2% ~ N(0,1), rho(Ad) < 1), N={N}: "
+                           f"on-device condensing + setup + one controllerStep each",
+               "batch_per_gpu": B, "horizon": N, "parallelism": f"dp{world}"} if perplant else
+              {"workload": f"cfg5: {B} plants per GPU x {a.ctrl_steps} warm-started control steps, simulated plant "
+                           f"(noise std {a.noise}, X0 ~ N(0, {workload.STREAM_X_SCALE}^2 diag(.1,.1,.05,.5)), U0 = 0), "
+                           f"hipGraph-replayed, N={N}",
+               "batch_per_gpu": B, "horizon": N, "ctrl_steps": a.ctrl_steps, "parallelism": f"dp{world}"})
+    rec = _header(a, world, total_qps, wall, a.dtype, "QP solves/sec (n_x=4, n_u=1, N=20 batch)",
+                  "synthetic (counter-based X ~ N(0, diag(.1,.1,.05,.5)), U ~ U(-1,1); reference plant config)"
+                  if not stream_mode else "synthetic (counter-based initial states and plant noise; reference plant config)",
+                  config)
+    rec["roofline"] = {
+        "bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS[a.dtype], "unit": "TFLOP/s",
+        "frac": achieved / PEAK_TFLOPS[a.dtype], "traffic": traffic_per_solve(a.dtype, B, N) if not stream_mode else None,
+        "kernel": f"admm_{kind}_kernel{' (paired loop)' if paired else ''} (all launches of "
+                  f"{'the step' if not stream_mode else 'the control steps'})",
+        "kernel_ms": kern_ms, "flops_per_step": flops,
+        "dense_equivalent": {"flops_per_step": flops_dense, "achieved": flops_dense / (kern_ms * 1e-3) / 1e12,
+                             "frac": flops_dense / (kern_ms * 1e-3) / 1e12 / PEAK_TFLOPS[a.dtype]},
+        "flops_note": "algorithmic: sum over QPs of iters*F_iter + checks*F_check + front end (SURVEY §8d, DESIGN §4.1), "
+                      "actual per-QP iteration counts"
+                      + ("; F_iter and F_check count the m/2-row products the paired loop performs "
+                         "(dense_equivalent: the dense 4nm count)" if paired else "")
+                      + ("; stream: every control step's iterations, accumulated on the device" if stream_mode else "")}
+    rec["iters"] = {"mean": float(iters.mean()), "max": int(iters.max()), "solved_frac": solved}
+    if stream_mode:
+        rec["iters"]["stream_total_mean"] = float(it_total.mean())
+        rec["iters"]["stream_unsolved_steps"] = int(solver.stream_unsolved())
+        rec["iters"]["final_max_abs_X"] = float(X_d.abs().max().item())
+    rec["collective"] = _collective(dist, world, got)
     if perplant:
         # The step is two stages of different character: per-plant condensing + setup (fp64 VALU/LDS,
-        # one wave per plant; the dominant stage) and the one-QP-per-wave ADMM solve (VALU, T = dtype).
-        # Each is priced against its own vector peak; the timed span of the setup stage includes the
-        # host read-back of the setup status word (mpcq_mpc_setup_plants_device synchronises once).
+        # one wave per plant) and the one-QP-per-wave ADMM solve (VALU, T = dtype).  Each is priced
+        # against its own vector peak; the timed span of the setup stage includes the host read-back
+        # of the setup status word (mpcq_mpc_setup_plants_device synchronises once).
+        setup_flops = B * workload.flops_plant_setup(N, 2 * N)
         rec["roofline"] = {"bound": "valu", "achieved": setup_flops / (setup_ms * 1e-3) / 1e12,
                            "peak": PEAK_TFLOPS["f64"], "unit": "TFLOP/s",
                            "frac": setup_flops / (setup_ms * 1e-3) / 1e12 / PEAK_TFLOPS["f64"], "traffic": None,
                            "kernel": "condense_wave_kernel + setup_wave_kernel (fp64 vector peak)",
                            "kernel_ms": setup_ms, "flops_per_step": setup_flops,
                            "flops_note": "algorithmic per plant (SURVEY §8d): F_condense + Ruiz + one LDL of the "
-                                         "KKT system; the eigen-basis setup's extra work is not credited"}
+                                         "KKT system"}
         rec["stages"] = {"setup_ms": setup_ms, "solve_ms": solve_ms, "step_ms": kern_ms,
                          "solve_roofline": {"bound": "valu", "achieved": flops / (solve_ms * 1e-3) / 1e12,
                                             "peak": PEAK_TFLOPS[a.dtype], "unit": "TFLOP/s",
                                             "frac": flops / (solve_ms * 1e-3) / 1e12 / PEAK_TFLOPS[a.dtype],
                                             "kernel": "admm_wave_kernel", "flops_per_step": flops}}
-    if a.cpu_seconds > 0 and perplant:
-        rec["cpu_baseline"] = cpu_baseline_plants(plant, Ad, Bd, N, X, U, a.cpu_seconds, a.cpu_threads)
-    elif a.cpu_seconds > 0 and not stream_mode:
-        rec["cpu_baseline"] = cpu_baseline(ops, N, X, U, a.cpu_seconds, a.cpu_threads)
-    print(json.dumps(rec))
-    if dist:
-        dist.destroy_process_group()
+    if a.cpu_seconds > 0 and not stream_mode:
+        import oracle
+
+        if perplant:
+            run = lambda n, t: oracle.plants_step(plant, Ad[:n], Bd[:n], X[:n], U[:n], N, nthreads=t)  # noqa: E731
+            rec["cpu_baseline"], ns, (U_ref, st_ref, it_ref) = cpu_baseline(
+                "port", run, 256, B, a.cpu_seconds, a.cpu_threads,
+                "oracle/mpc_batch.c condense + osqp_dense.c setup + one controllerStep per plant")
+            x_ref = (U_ref - U[:ns])[:, None]
+        else:
+            q0 = np.zeros(N)
+            q, u = oracle.gradient(ops, X, U), oracle.upper_bound(ops, X, U)
+            run = lambda n, t: oracle.batch_solve(ops["P"], ops["A"], q0, l, u0, q[:n], u[:n], nthreads=t)  # noqa: E731
+            rec["cpu_baseline"], ns, (x_ref, st_ref, it_ref, _) = cpu_baseline(
+                "port", run, 256, B, a.cpu_seconds, a.cpu_threads, "oracle/osqp_dense.c (OSQP-0.6 restatement)")
+        du = U_d[:ns].cpu().numpy() - U[:ns]
+        rec["parity"] = _parity(du, iters[:ns], x_ref, it_ref, st_ref)
+        if perplant:
+            rec["parity"].pop("max_rel_du0")  # (the per-plant oracle returns U only)
+    return rec
 
 
 if __name__ == "__main__":

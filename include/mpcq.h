@@ -128,8 +128,9 @@ int mpcq_get_scaling(mpcq_ctx *ctx, double *D, double *E, double *c); /* plant 0
 
 /* Device path the next solve takes (no OSQP counterpart; for benchmarks and tests):
  * *kind = MPCQ_PATH_TILE (shared plant, MFMA tile kernel + one-QP-per-wave tail), MPCQ_PATH_WAVE
- * (one QP per wave) or MPCQ_PATH_LANE (one QP per lane); *paired = 1 when the tile kernel runs its
- * paired loop (rows n + j of A are the negated rows j: the condensed-MPC constraint matrix). */
+ * (one QP per wave: per-plant contexts, and shared-plant batches under 8,192 QPs) or MPCQ_PATH_LANE
+ * (one QP per lane); *paired = 1 when the tile kernel runs its paired loop (rows n + j of A are the
+ * negated rows j: the condensed-MPC constraint matrix). */
 #define MPCQ_PATH_TILE 0
 #define MPCQ_PATH_WAVE 1
 #define MPCQ_PATH_LANE 2
@@ -171,6 +172,10 @@ int mpcq_mpc_simulate_device(mpcq_ctx *ctx, double *X_dev, const double *U_dev, 
 int mpcq_mpc_run_device(mpcq_ctx *ctx, double *X_dev, double *U_dev, double xref, int steps,
                         unsigned long long seed, long long first_qp, long long first_step,
                         double noise_std, void *stream);
+/* Per-QP counters of the last mpcq_mpc_run_device call (host arrays of `batch` ints, synchronises):
+ * the ADMM iterations of all its control steps, and the steps whose solve did not end SOLVED
+ * (controllerStep returning false, :102, where the reference's loop would exit, solver.cpp:50). */
+int mpcq_mpc_stream_counters(mpcq_ctx *ctx, int *iters, int *unsolved);
 
 /* Condensed-QP construction on device `device` for n_plants SISO plants (ModelPredictiveControlAPI
  * setTransformations / setLL / setLiftedCosts / setH / setFVars / setLinearConstraints /

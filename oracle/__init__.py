@@ -49,6 +49,7 @@ class Info(C.Structure):
         ("iter", C.c_int), ("status", C.c_int), ("rho_updates", C.c_int),
         ("pri_res", C.c_double), ("dua_res", C.c_double),
         ("rho_estimate", C.c_double), ("rho", C.c_double),
+        ("margin", C.c_double),  # smallest |ln(value / threshold)| of the solve's schedule decisions
     ]
 
 
@@ -108,7 +109,7 @@ def lib() -> C.CDLL:
     L.ora_get_iterates.argtypes = [C.c_void_p, dp, dp, dp]
     L.ora_batch_solve.restype = C.c_int
     L.ora_batch_solve.argtypes = [C.c_int, C.c_int, dp, dp, dp, dp, dp, C.POINTER(Settings),
-                                  C.c_int, dp, dp, dp, ip, ip, dp, C.c_int]
+                                  C.c_int, dp, dp, dp, ip, ip, dp, C.c_int, dp]
     L.ora_condense.argtypes = [C.POINTER(_Plant), C.POINTER(_Ops)]
     L.ora_condense.restype = C.c_int
     L.ora_matpow.argtypes = [C.c_int, dp, C.c_int, dp]
@@ -317,8 +318,10 @@ class Solver:
         return x, z, y
 
 
-def batch_solve(P, A, q0, l, u0, q, u, settings: Settings | None = None, nthreads: int = 0):
-    """Shared-template batch: setup(P,q0,A,l,u0) then per QP update q[b], u[b] and solve."""
+def batch_solve(P, A, q0, l, u0, q, u, settings: Settings | None = None, nthreads: int = 0,
+                margins: bool = False):
+    """Shared-template batch: setup(P,q0,A,l,u0) then per QP update q[b], u[b] and solve.
+    Returns (x, status, iter, rho) and, with ``margins``, each QP's decision margin (Info.margin)."""
     P, A, q0, l, u0 = map(_c64, (P, A, q0, l, u0))
     q, u = _c64(q), _c64(u)
     n, m, B = P.shape[0], A.shape[0], q.shape[0]
@@ -327,11 +330,12 @@ def batch_solve(P, A, q0, l, u0, q, u, settings: Settings | None = None, nthread
     st = np.zeros(B, dtype=np.int32)
     it = np.zeros(B, dtype=np.int32)
     rho = np.zeros(B)
+    mg = np.zeros(B)
     rc = lib().ora_batch_solve(n, m, _dp(P), _dp(A), _dp(q0), _dp(l), _dp(u0), C.byref(s), B,
-                               _dp(q), _dp(u), _dp(x), _ip(st), _ip(it), _dp(rho), nthreads)
+                               _dp(q), _dp(u), _dp(x), _ip(st), _ip(it), _dp(rho), nthreads, _dp(mg))
     if rc < 0:
         raise ValueError("ora_batch_solve: setup rejected the data")
-    return x, st, it, rho
+    return (x, st, it, rho, mg) if margins else (x, st, it, rho)
 
 
 def plants_step(plant: dict, Ad, Bd, X, U, N: int, s_rows: int = 10, xref: float = 0.0,

@@ -443,11 +443,22 @@ static int is_dual_infeasible(ora_work *w, double eps)
     return 0;
 }
 
+/* decision margin (diagnostics only): |ln(value / threshold)| of one comparison */
+static double log_margin(double v, double thr)
+{
+    return (v > 0 && thr > 0) ? fabs(log(v / thr)) : INFINITY;
+}
+static void note_margin(ora_work *w, double r)
+{
+    if (r < w->info.margin) w->info.margin = r;
+}
+
 static int check_termination(ora_work *w, int approximate)
 {
     double eps_abs = w->set.eps_abs, eps_rel = w->set.eps_rel;
     double eps_pinf = w->set.eps_prim_inf, eps_dinf = w->set.eps_dual_inf;
     int prim_ok = 0, dual_ok = 0, prim_inf = 0, dual_inf = 0;
+    double mp = INFINITY;
     if (w->info.pri_res > OSQP_INFTY || w->info.dua_res > OSQP_INFTY) {
         w->info.status = ORA_NON_CVX;
         return 1;
@@ -459,12 +470,18 @@ static int check_termination(ora_work *w, int approximate)
         prim_ok = 1;
     } else {
         double ep = compute_pri_tol(w, eps_abs, eps_rel);
+        mp = log_margin(w->info.pri_res, ep);
         if (w->info.pri_res < ep) prim_ok = 1;
         else prim_inf = is_primal_infeasible(w, eps_pinf);
     }
     double ed = compute_dua_tol(w, eps_abs, eps_rel);
     if (w->info.dua_res < ed) dual_ok = 1;
     else dual_inf = is_dual_infeasible(w, eps_dinf);
+    if (!approximate) {  /* the solved test flips only when every failing comparison flips */
+        const double md = log_margin(w->info.dua_res, ed);
+        if (prim_ok && dual_ok) note_margin(w, fmin(mp, md));
+        else note_margin(w, fmax(prim_ok ? 0.0 : mp, dual_ok ? 0.0 : md));
+    }
 
     if (prim_ok && dual_ok) {
         w->info.status = approximate ? ORA_SOLVED_INACCURATE : ORA_SOLVED;
@@ -521,6 +538,8 @@ static int adapt_rho(ora_work *w)
 {
     double rho_new = compute_rho_estimate(w);
     w->info.rho_estimate = rho_new;
+    note_margin(w, fmin(log_margin(rho_new, w->set.rho * w->set.adaptive_rho_tolerance),
+                        log_margin(rho_new, w->set.rho / w->set.adaptive_rho_tolerance)));
     if (rho_new > w->set.rho * w->set.adaptive_rho_tolerance ||
         rho_new < w->set.rho / w->set.adaptive_rho_tolerance) {
         int e = osqp_update_rho(w, rho_new);
@@ -569,6 +588,7 @@ static void swap(double **a, double **b)
 int ora_solve(ora_work *w)
 {
     int iter, can_check = 0;
+    w->info.margin = INFINITY;
     if (!w->set.warm_start) ora_cold_start(w);
     for (iter = 1; iter <= w->set.max_iter; iter++) {
         swap(&w->x, &w->x_prev);
@@ -779,7 +799,7 @@ void ora_get_iterates(const ora_work *w, double *x, double *z, double *y)
 int ora_batch_solve(int n, int m, const double *P, const double *A, const double *q0,
                     const double *l, const double *u0, const ora_settings *s, int batch,
                     const double *q, const double *u, double *x, int *status, int *iters,
-                    double *rho_out, int nthreads)
+                    double *rho_out, int nthreads, double *margin_out)
 {
     ora_work *tmpl = ora_setup(n, m, P, q0, A, l, u0, s);
     if (!tmpl) return -1;
@@ -809,6 +829,7 @@ int ora_batch_solve(int n, int m, const double *P, const double *A, const double
             if (status) status[b] = w->info.status;
             if (iters) iters[b] = w->info.iter;
             if (rho_out) rho_out[b] = w->set.rho;
+            if (margin_out) margin_out[b] = w->info.margin;
         }
         ora_cleanup(w);
     }

@@ -48,6 +48,9 @@ typedef struct {
 typedef struct {
     int iter, status, rho_updates;
     double pri_res, dua_res, rho_estimate, rho;
+    /* smallest |ln(value / threshold)| over this solve's decisions (termination tests and
+     * adaptive-rho tests): how far the iteration schedule is from flipping (test diagnostics) */
+    double margin;
 } ora_info;
 
 typedef struct ora_work ora_work;
@@ -79,12 +82,13 @@ void ora_get_iterates(const ora_work *w, double *x, double *z, double *y);
 
 /* Batch driver used by tests and bench.py's cpu_baseline: one shared (P, A, l, setup q0/u0)
  * template; for every QP b: fresh copy of the template, update_lin_cost(q[b]),
- * update_upper_bound(u[b]), solve.  Writes x (batch*n), status, iter, final rho.
+ * update_upper_bound(u[b]), solve.  Writes x (batch*n), status, iter, final rho, decision margin
+ * (each output may be NULL except x).
  * nthreads <= 0 => OpenMP default.  Returns the number of QPs whose update failed. */
 int ora_batch_solve(int n, int m, const double *P, const double *A, const double *q0,
                     const double *l, const double *u0, const ora_settings *s, int batch,
                     const double *q, const double *u, double *x, int *status, int *iters,
-                    double *rho_out, int nthreads);
+                    double *rho_out, int nthreads, double *margin_out);
 
 #ifdef __cplusplus
 }

@@ -198,6 +198,20 @@ class BatchSolver:
                                               int(steps), seed, first_qp, first_step, float(noise_std),
                                               C.c_void_p(stream)), "mpcq_mpc_run_device")
 
+    def stream_counters(self):
+        """Per-QP (iterations, unsolved steps) accumulated over the last mpc_run_device call."""
+        it = np.empty(self.batch, dtype=np.int32)
+        un = np.empty(self.batch, dtype=np.int32)
+        _capi.check(lib().mpcq_mpc_stream_counters(self._ctx, it.ctypes.data_as(C.POINTER(C.c_int)),
+                                                   un.ctypes.data_as(C.POINTER(C.c_int))), "mpcq_mpc_stream_counters")
+        return it, un
+
+    def stream_iterations(self) -> np.ndarray:
+        return self.stream_counters()[0]
+
+    def stream_unsolved(self) -> int:
+        return int(self.stream_counters()[1].sum())
+
     def mpc_setup_plants_device(self, nx: int, s_rows: int, Ad_ptr: int, Bd_ptr: int, Cd_ptr: int, K_ptr: int,
                                 Q_ptr: int, R_ptr: int, RD_ptr: int, stream: int | None = None) -> None:
         """Condense and set up every plant on the device from device-resident plant data (fp64,

@@ -10,6 +10,25 @@
 
 using mpcq::Matrix;
 
+namespace {
+// "<name> rows: r\t<name> cols: c" / "<name>:" / matrix / blank line, as the reference's -v dumps
+// print every operator (ModelPredictiveControlAPI.cpp:122-132 and the other set* builders).
+void dump(const char *name, const Matrix &m, const char *cols_name = nullptr)
+{
+    std::cout << name << " rows: " << m.rows() << "\t" << (cols_name ? cols_name : name) << " cols: " << m.cols()
+              << std::endl;
+    std::cout << name << ":" << std::endl << m << std::endl << std::endl;
+}
+
+Matrix matpow(const Matrix &A, int k)
+{
+    Matrix r(A.rows(), A.cols());
+    for (int i = 0; i < A.rows(); i++) r(i, i) = 1.0;
+    for (int t = 0; t < k; t++) r = r * A;
+    return r;
+}
+}  // namespace
+
 ModelPredictiveControlAPI::ModelPredictiveControlAPI(bool verbose_, const std::string &config, int N, int device)
     : solver(device), horizon(N), device_(device)
 {
@@ -17,7 +36,8 @@ ModelPredictiveControlAPI::ModelPredictiveControlAPI(bool verbose_, const std::s
     verbose = verbose_;
     solverFlag = true;
     std::ifstream file(config);  // CWD-relative by default, like the reference (:12)
-    if (!file) throw json_lite::error("parse_error: cannot open " + config);
+    if (!file)  // json::parse of an unopened stream sees an empty input (:13)
+        throw json_lite::detail::parse_error::create(101, 1, "syntax error while parsing value - unexpected end of input (" + config + ")");
     std::stringstream ss;
     ss << file.rdbuf();
     cfg = json_lite::parse(ss.str());
@@ -80,7 +100,13 @@ void ModelPredictiveControlAPI::setSystemVars()
     Bd = from_json(cfg["Bd"], N_S, N_C);
     Cd = from_json(cfg["Cd"], N_O, N_S);
     Dd = from_json(cfg["Dd"], N_O, N_C);
-    if (verbose) std::cout << "[MPC API]\tSystem variables created." << std::endl;
+    if (verbose) {
+        std::cout << "[MPC API]\tSystem variables created." << std::endl;
+        dump("Ad", Ad);
+        dump("Bd", Bd);
+        dump("Cd", Cd);
+        dump("Dd", Dd);
+    }
 }
 
 void ModelPredictiveControlAPI::setCosts()
@@ -88,7 +114,12 @@ void ModelPredictiveControlAPI::setCosts()
     Q = from_json(cfg["Q"], N_O, N_O);
     R = from_json(cfg["R"], N_O, N_O);
     RD = from_json(cfg["RD"], N_O, N_O);
-    if (verbose) std::cout << "[MPC API]\tSet Q, R, and RD matrices created." << std::endl;
+    if (verbose) {
+        std::cout << "[MPC API]\tSet Q, R, and RD matrices created." << std::endl;
+        dump("Q", Q);
+        dump("R", R);
+        dump("RD", RD);
+    }
 }
 
 void ModelPredictiveControlAPI::setLiftedCosts()
@@ -96,7 +127,12 @@ void ModelPredictiveControlAPI::setLiftedCosts()
     Qbar = blkdiag(Q, horizon);
     Rbar = blkdiag(R, horizon);
     RbarD = blkdiag(RD, horizon);
-    if (verbose) std::cout << "[MPC API]\tLifted weight matrices created." << std::endl;
+    if (verbose) {
+        std::cout << "[MPC API]\tLifted weight matrices created." << std::endl;
+        dump("Qbar", Qbar);
+        dump("Rbar", Rbar);
+        dump("RbarD", RbarD);
+    }
 }
 
 // The condensed operators come from the device kernel (mpcq_condense), built once here and
@@ -124,22 +160,76 @@ void ModelPredictiveControlAPI::condense_on_device()
     condensed_ = true;
 }
 
+// The -v dump of setTransformations (:210-243) prints intermediate matrices the QP never reads (the
+// device kernel builds every operator it does read).  They are formed here for printing only.
+void ModelPredictiveControlAPI::transformations_for_dump(Matrix &CAB, Matrix &CAiB, Matrix &CAB_full,
+                                                         Matrix &Su_full, Matrix &Su_full1) const
+{
+    const int N = horizon;
+    CAB = Matrix(N, 1);
+    CAiB = Matrix(N_S, N_O);
+    CAB_full = Matrix(N_S * N, N_O);
+    Sx = Matrix(N, N_S);
+    for (int i = 0; i < N; i++) {
+        const Matrix Ai = matpow(Ad, i), Ai1 = Ai * Ad;
+        const Matrix cx = Cd * Ai1, cab = Cd * Ai * Bd, aib = Ai * Bd;
+        for (int c = 0; c < N_S; c++) Sx(i, c) = cx(0, c);
+        CAB(i) = cab(0, 0);
+        for (int r = 0; r < N_S; r++) CAiB(r) += aib(r, 0);
+        for (int r = 0; r < N_S; r++) CAB_full(N_S * i + r) = CAiB(r);
+    }
+    Su = Matrix(N, N);  // strict upper triangle never written (:197-204): zero here
+    Su_full = Matrix(N_S * N, N);
+    for (int i = 0; i < N; i++)
+        for (int j = 0; j <= i; j++) {
+            double acc = 0.0;
+            for (int k = 0; k <= i - j; k++) acc += CAB(k);
+            Su(i, j) = acc;
+            for (int r = 0; r < N_S; r++) Su_full(N_S * i + r, j) = CAB_full(N_S * (i - j) + r);
+        }
+    Su1 = Matrix(N, N_O);
+    Su_full1 = Matrix(N_S * N, 1);
+    for (int i = 0; i < N; i++) Su1(i) = Su(i, 0);
+    for (int i = 0; i < N_S * N; i++) Su_full1(i) = Su_full(i, 0);
+}
+
 void ModelPredictiveControlAPI::setTransformations()
 {
     if (!condensed_) condense_on_device();
-    if (verbose) std::cout << "[MPC API]\tTransformation matrices created" << std::endl;
+    if (verbose) {
+        std::cout << "[MPC API]\tTransformation matrices created" << std::endl;
+        Matrix CAB, CAiB, CAB_full, Su_full, Su_full1;
+        transformations_for_dump(CAB, CAiB, CAB_full, Su_full, Su_full1);
+        dump("Sx", Sx);
+        dump("CAB", CAB);
+        dump("CAiB", CAiB);
+        dump("CAB_full", CAB_full);
+        dump("S", S);
+        dump("Su", Su);
+        dump("Su1", Su1);
+        dump("Su_full", Su_full, "Su1");  // (the reference labels these columns "Su1", :235,238)
+        dump("Su_full1", Su_full1, "Su1");
+        dump("Sbar", Sbar);
+    }
 }
 
 void ModelPredictiveControlAPI::setH()
 {
     if (!condensed_) condense_on_device();
-    if (verbose) std::cout << "[MPC API]\tHessian H created." << std::endl;
+    if (verbose) {
+        std::cout << "[MPC API]\tHessian H created." << std::endl;
+        dump("H", H);
+    }
 }
 
 void ModelPredictiveControlAPI::setLu()
 {
     Lu = Matrix(horizon, 1);  // (mpcWindow - i + 2), unused by the QP (:274-279)
     for (int i = 0; i < horizon; i++) Lu(i) = horizon - i + 2;
+    if (verbose) {
+        std::cout << "[MPC API]\tLu created." << std::endl;
+        dump("Lu", Lu);
+    }
 }
 
 void ModelPredictiveControlAPI::setLL()
@@ -147,18 +237,30 @@ void ModelPredictiveControlAPI::setLL()
     LL = Matrix(horizon, horizon);
     for (int i = 0; i < horizon; i++)
         for (int j = 0; j <= i; j++) LL(i, j) = 1.0;
+    if (verbose) {
+        std::cout << "[MPC API]\tLL created." << std::endl;
+        dump("LL", LL);
+    }
 }
 
 void ModelPredictiveControlAPI::setFVars()
 {
     if (!condensed_) condense_on_device();
-    if (verbose) std::cout << "[MPC API]\tComponents of F created." << std::endl;
+    if (verbose) {
+        std::cout << "[MPC API]\tComponents of F created." << std::endl;
+        dump("Fu", Fu);
+        dump("Fr", Fr);
+        dump("Fx", Fx);
+    }
 }
 
 void ModelPredictiveControlAPI::setLinearConstraints()
 {
     if (!condensed_) condense_on_device();
-    if (verbose) std::cout << "[MPC API]\tLinear constraints matrix created." << std::endl;
+    if (verbose) {
+        std::cout << "[MPC API]\tLinear constraints matrix created." << std::endl;
+        dump("Gbar", Gbar);
+    }
 }
 
 void ModelPredictiveControlAPI::setUpperBound()
@@ -183,7 +285,7 @@ void ModelPredictiveControlAPI::setF()
 void ModelPredictiveControlAPI::updateRef(double pos_ref)
 {
     ref = Matrix(1, horizon, pos_ref);
-    if (verbose) std::cout << "[MPC API]\tref: " << pos_ref << std::endl;
+    if (verbose) std::cout << "[MPC API]\tref: " << ref << std::endl;
 }
 
 bool ModelPredictiveControlAPI::controllerStep()
@@ -214,51 +316,54 @@ Matrix ModelPredictiveControlAPI::blkdiag(const Matrix &a, int count)
     return b;
 }
 
-// from_json shape rules of the reference (:418-489): scalar, row/column vector or matrix.
-Matrix ModelPredictiveControlAPI::from_json(const json_lite::Value &j, int rows, int cols)
+// from_json (:418-489): a scalar, a row or column vector, or a matrix (array of rows), shape-checked
+// against (rows, cols); every failure prints the reference's stderr line where it has one and throws
+// json_lite's type_error::create(0, "") as the reference throws nlohmann's.  Element conversion
+// follows json's: a non-number element throws type_error 302, a scalar row indexed as an array 304.
+Matrix ModelPredictiveControlAPI::from_json(const json_lite::Value &jsonObject, int rows, int cols)
 {
-    std::vector<const json_lite::Value *> flat;
-    json_lite::Value arr;
-    if (j.is_array()) {
-        if (j.empty()) return Matrix(rows, cols);
-        arr = j;
-    } else if (j.is_number()) {
-        arr.kind = json_lite::Value::Array;
-        arr.arr.push_back(j);
+    using json_lite::Value;
+    using json_lite::detail::type_error;
+    Value jsonArray;
+    jsonArray.kind = Value::Array;
+    if (jsonObject.is_array()) {
+        if (jsonObject.empty()) return Matrix(rows, cols);  // (:425-428; Eigen leaves it uninitialised)
+        jsonArray = jsonObject;
+    } else if (jsonObject.is_number()) {
+        jsonArray.arr.push_back(jsonObject);
     } else {
-        throw json_lite::error("type_error: expected a number or an array");
+        throw type_error::create(0, "");  // (:437)
     }
-    std::vector<std::vector<double>> aoa;
-    if (arr.arr.front().is_array()) {
-        for (const auto &row : arr.arr) {
-            std::vector<double> r;
-            if (!row.is_array()) throw json_lite::error("type_error: mixed rows");
-            for (const auto &v : row.arr) r.push_back(v.get_double());
-            aoa.push_back(r);
-        }
+    Value aoa;
+    aoa.kind = Value::Array;
+    if (jsonArray.arr.front().is_array()) {
+        aoa = jsonArray;  // provided matrix
     } else if (rows == 1) {
-        std::vector<double> r;
-        for (const auto &v : arr.arr) r.push_back(v.get_double());
-        aoa.push_back(r);
+        aoa.arr.push_back(jsonArray);  // row vector
     } else if (cols == 1) {
-        for (const auto &v : arr.arr) aoa.push_back({v.get_double()});
+        for (const Value &v : jsonArray.arr) {  // column vector
+            Value row;
+            row.kind = Value::Array;
+            row.arr.push_back(v);
+            aoa.arr.push_back(row);
+        }
     } else {
         std::cerr << "Expected a matrix, received a vector." << std::endl;
-        throw json_lite::error("type_error: expected a matrix");
+        throw type_error::create(0, "");  // (:460-461)
     }
-    const int pr = (int)aoa.size(), pc = (int)aoa.front().size();
+    const int pr = (int)aoa.size(), pc = (int)aoa.arr.front().size();
     if ((rows >= 0 && pr != rows) || (cols >= 0 && pc != cols)) {
         std::cerr << "Expected matrix of size " << rows << "x" << cols << ", received matrix of size " << pr << "x" << pc
                   << "." << std::endl;
-        throw json_lite::error("type_error: size mismatch");
+        throw type_error::create(0, "");  // (:471)
     }
     Matrix m(pr, pc);
     for (int r = 0; r < pr; r++) {
-        if ((int)aoa[r].size() != pc) {
+        if ((int)aoa.at(r).size() != pc) {
             std::cerr << "Unconsistent matrix size: some rows have different number of columns." << std::endl;
-            throw json_lite::error("type_error: ragged rows");
+            throw type_error::create(0, "");  // (:480)
         }
-        for (int c = 0; c < pc; c++) m(r, c) = aoa[r][c];
+        for (int c = 0; c < pc; c++) m(r, c) = aoa.at(r).at(c).get_double();
     }
     return m;
 }

@@ -47,7 +47,8 @@ public:
     // system matrices (ModelPredictiveControlAPI.h:148-200)
     mpcq::Matrix Ad, Bd, Cd, Dd;
     mpcq::Matrix Q, R, RD, Qbar, Rbar, RbarD;
-    mpcq::Matrix S, Sbar, W0, Gbar, Sx, Su, Su1, LL, Lu;
+    mpcq::Matrix S, Sbar, W0, Gbar, LL, Lu;
+    mutable mpcq::Matrix Sx, Su, Su1;  // printed by the -v dump only (the device kernel forms the QP)
     mpcq::Matrix X, U, ref, K, Ku;
     double xref = 0.0;
     mpcq::Matrix H, Fu, Fr, Fx, f, lb, ub;
@@ -62,6 +63,8 @@ public:
 
 private:
     void condense_on_device();
+    void transformations_for_dump(mpcq::Matrix &CAB, mpcq::Matrix &CAiB, mpcq::Matrix &CAB_full, mpcq::Matrix &Su_full,
+                                  mpcq::Matrix &Su_full1) const;
     bool condensed_ = false;
     int device_;
 };

@@ -1,7 +1,9 @@
 // solvempc_amd/cpp/mpcq_solver.cpp — osqp-eigen-shaped single-QP solver over the C ABI.
 #include "mpcq_solver.hpp"
 
+#include <algorithm>
 #include <cstdio>
+#include <sstream>
 
 namespace mpcq {
 
@@ -19,6 +21,48 @@ Matrix Matrix::from_row_major(int rows, int cols, const double *p)
     for (int i = 0; i < rows; i++)
         for (int j = 0; j < cols; j++) m(i, j) = p[(size_t)i * cols + j];
     return m;
+}
+
+Matrix Matrix::transpose() const
+{
+    Matrix t(c_, r_);
+    for (int i = 0; i < r_; i++)
+        for (int j = 0; j < c_; j++) t(j, i) = (*this)(i, j);
+    return t;
+}
+
+Matrix Matrix::operator*(const Matrix &b) const
+{
+    Matrix p(r_, b.c_);
+    for (int i = 0; i < r_; i++)
+        for (int j = 0; j < b.c_; j++) {
+            double s = 0.0;
+            for (int k = 0; k < c_; k++) s += (*this)(i, k) * b(k, j);
+            p(i, j) = s;
+        }
+    return p;
+}
+
+std::ostream &operator<<(std::ostream &os, const Matrix &m)
+{
+    if (m.size() == 0) return os;
+    std::streamsize width = 0;
+    for (int j = 0; j < m.cols(); j++)
+        for (int i = 0; i < m.rows(); i++) {
+            std::ostringstream one;
+            one.copyfmt(os);
+            one << m(i, j);
+            width = std::max<std::streamsize>(width, (std::streamsize)one.str().size());
+        }
+    for (int i = 0; i < m.rows(); i++) {
+        for (int j = 0; j < m.cols(); j++) {
+            if (j) os << ' ';
+            os.width(width);
+            os << m(i, j);
+        }
+        if (i + 1 < m.rows()) os << '\n';
+    }
+    return os;
 }
 
 // osqp-eigen's Data setters check the sizes against setNumberOf* and return false on mismatch.

@@ -12,6 +12,7 @@
 // Eigen is not part of this build: matrices are mpcq::Matrix (column-major, like Eigen's default).
 #pragma once
 
+#include <ostream>
 #include <string>
 #include <vector>
 
@@ -39,11 +40,18 @@ public:
     // row-major copy (the C ABI's layout)
     std::vector<double> row_major() const;
     static Matrix from_row_major(int rows, int cols, const double *p);
+    Matrix transpose() const;
+    Matrix operator*(const Matrix &b) const;
 
 private:
     int r_ = 0, c_ = 0;
     std::vector<double> v_;
 };
+
+// Printed as Eigen's default IOFormat prints a matrix (the reference's -v dumps,
+// ModelPredictiveControlAPI.cpp:118-176,210-243,265-321): every coefficient right-aligned to the
+// widest one at the stream's precision, columns separated by one space, rows by newlines.
+std::ostream &operator<<(std::ostream &os, const Matrix &m);
 
 using Vector = std::vector<double>;
 

@@ -3,9 +3,10 @@
 // format: every input line is one "serial message"; lines longer than 30 bytes are parsed as
 // "dt x0 x1 x2 x3" into float (SerialPort.cpp:106-139, incl. its float[5] buffer), shorter ones are
 // bad reads that resend the last U (solver.cpp:69-73).  Each output line is what writePort sends:
-// the first sizeof(char*) = 8 characters of std::to_string(U) (SerialPort.cpp:162-166).
+// the first sizeof(char*) = 8 characters of std::to_string(U) (SerialPort.cpp:162-166), one per line,
+// to stdout or to the -o file (the "serial port" side, kept apart from the -v log).
 //
-//   solvempc [-v] [-c ./config/MPC_API.json] [-N 15] [-i messages.txt]   (stdin by default)
+//   solvempc [-v] [-c ./config/MPC_API.json] [-N 15] [-i messages.txt] [-o wire.txt]
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
@@ -48,12 +49,20 @@ int main(int argc, char **argv)
     const char *cfg = getCmdOption(argv, argv + argc, "-c");
     const char *hz = getCmdOption(argv, argv + argc, "-N");
     const char *in = getCmdOption(argv, argv + argc, "-i");
+    const char *outp = getCmdOption(argv, argv + argc, "-o");
     ModelPredictiveControlAPI mpc(verbose, cfg ? cfg : "./config/MPC_API.json", hz ? std::atoi(hz) : mpcWindow);
     if (!mpc.solverFlag) return 1;
 
     std::ifstream file;
     if (in) file.open(in);
+    if (in && !file) {
+        std::cerr << "[solveMPC]\tcannot open " << in << std::endl;
+        return 1;
+    }
     std::istream &src = in ? static_cast<std::istream &>(file) : std::cin;
+    std::ofstream wfile;
+    if (outp) wfile.open(outp);
+    std::ostream &wire_out = outp ? static_cast<std::ostream &>(wfile) : std::cout;
     std::cout << "----------------------------------------------------\n"
                  "-------------- Entering control loop. --------------\n"
                  "----------------------------------------------------" << std::endl;
@@ -61,14 +70,15 @@ int main(int argc, char **argv)
     double dt_msg = 0.0;  // readPort takes dt by value: mpc.dt never changes (SerialPort.cpp:142)
     while (std::getline(src, line)) {
         if (parse_message(line, dt_msg, mpc.X)) {
+            if (mpc.verbose)  // (SerialPort.cpp:150; the message keeps its newline)
+                std::cout << "\n[SerialPort]\tRead " << line.size() + 1 << " bytes. Received message: " << line << "\n";
             if (!mpc.controllerStep()) return 1;
-            if (mpc.verbose) {
-                std::cout << "[solveMPC]\tCurrent state: " << mpc.X(0) << " " << mpc.X(1) << " " << mpc.X(2) << " "
-                          << mpc.X(3) << std::endl;
-                std::cout << "[solveMPC]\tControl output: " << mpc.U(0) << std::endl;
+            if (mpc.verbose) {  // (solver.cpp:53-57)
+                std::cout << "[solveMPC]\tCurrent state: " << mpc.X.transpose() << std::endl;
+                std::cout << "[solveMPC]\tControl output: " << mpc.U.transpose() << std::endl;
             }
         }
-        std::cout << wire(mpc.U(0)) << std::endl;  // writePort(mpc.U)
+        wire_out << wire(mpc.U(0)) << std::endl;  // writePort(mpc.U); a bad read resends the last U (:69-73)
     }
     return 0;
 }

@@ -467,6 +467,10 @@ void admm_lane_kernel(AdmmArgs<T> a)
     a.status[b] = status;
     a.iter[b] = it;
     a.rho_out[b] = (double)rho;
+    if (a.it_acc) {
+        a.it_acc[b] += it;
+        a.uns_acc[b] += status != kSolved;
+    }
 }
 
 // osqp_warm_start: x^ = Dinv x, x' = W^-1 x^, z = A^ x^, y^ = c Einv y  (all QPs).  Cold path with

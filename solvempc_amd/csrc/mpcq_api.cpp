@@ -47,7 +47,11 @@ struct mpcq_ctx {
     mpcq_settings set{};
     int nc = 0, mc = 0;
     size_t ops_stride = 0;
-    bool setup_done = false, all_ineq = true, mpc_ready = false, lower_free = false, fresh = false;
+    // The formulation the context was last set up for: the generic / condensed-MPC operators
+    // (mpcq_setup, mpcq_mpc_setup_plants_device) or the MIMO operator blocks
+    // (mpcq_mimo_setup_plants_device).  Each entry point checks for the one it runs on.
+    enum class Mode { None, Generic, Mimo } mode = Mode::None;
+    bool all_ineq = true, mpc_ready = false, lower_free = false, fresh = false;
     bool paired = false;  // shared plant of the condensed-MPC shape (tile kernel's paired loop)
     // tile (MFMA) path: shared plant with a compiled (KN, KM) shape
     bool tile = false;
@@ -88,7 +92,10 @@ struct mpcq_ctx {
     // MIMO condensed MPC (mpcq_mimo.hip): per-plant operator block, dims
     double *d_mimo = nullptr;
     int mimo_N = 0, mimo_nx = 0, mimo_nu = 0, mimo_ny = 0, mimo_srows = 0, mimo_diag_k0 = 0;
-    bool mimo_ready = false, mimo_only = false;
+    bool mimo_only = false;  // n > 32 or m > 64 per plant: only the MIMO entry points serve it
+    // receding-horizon stream counters (mpcq_mpc_run_device): per-QP iterations and unsolved steps
+    int *d_it_acc = nullptr, *d_uns_acc = nullptr;
+    bool stream_acc = false;  // launches made inside mpcq_mpc_run_device accumulate into them
     // host copies of plant-0 scaling
     std::vector<double> hD, hE;
     double hc = 1.0;
@@ -153,7 +160,6 @@ mpcq::AdmmArgs<T> make_args(mpcq_ctx *c)
     const int ct = c->set.check_termination;
     a.adaptive_interval = c->set.adaptive_rho_interval ? c->set.adaptive_rho_interval : (ct ? 4 * ct : 100);
     a.all_ineq = c->all_ineq;
-    a.paired = c->paired && c->tile && std::strcmp(std::getenv("MPCQ_PAIRED") ? std::getenv("MPCQ_PAIRED") : "1", "0") != 0;
     a.lower_free = c->lower_free;
     a.q = c->d_q;
     a.u = c->d_u;
@@ -172,6 +178,8 @@ mpcq::AdmmArgs<T> make_args(mpcq_ctx *c)
     a.rho_out = c->d_rho;
     a.status = c->d_status;
     a.iter = c->d_iter;
+    a.it_acc = c->stream_acc ? c->d_it_acc : nullptr;
+    a.uns_acc = c->stream_acc ? c->d_uns_acc : nullptr;
     return a;
 }
 
@@ -214,11 +222,30 @@ bool lower_all_free_batch(const mpcq_ctx *c, const double *l)
     return true;
 }
 
-int check_ctx(mpcq_ctx *c, bool need_setup)
+enum Need { kNone, kGeneric, kAnySetup };
+
+// kGeneric: the generic / condensed-MPC operators (the generic kernels run on them); kAnySetup:
+// either formulation (result readers).  A MIMO-only context never passes kGeneric.
+int check_ctx(mpcq_ctx *c, Need need)
 {
     if (!c) return fail(MPCQ_ERR_ARG, "null context");
-    if (need_setup && !c->setup_done) return fail(MPCQ_ERR_ORDER, "mpcq_setup has not succeeded");
+    if (need == kGeneric && c->mimo_only)
+        return fail(MPCQ_ERR_ARG, "n > 32 or m > 64 per plant: this context is served by mpcq_mimo_* only");
+    if (need == kGeneric && c->mode != mpcq_ctx::Mode::Generic)
+        return fail(MPCQ_ERR_ORDER, c->mode == mpcq_ctx::Mode::Mimo
+                                        ? "the context was last set up by mpcq_mimo_setup_plants_device (MIMO)"
+                                        : "mpcq_setup has not succeeded");
+    if (need == kAnySetup && c->mode == mpcq_ctx::Mode::None) return fail(MPCQ_ERR_ORDER, "no setup has succeeded");
     HIPCHK(hipSetDevice(c->dims.device));
+    return MPCQ_OK;
+}
+
+// Generic entry points that only need the device and the generic buffers (no setup yet)
+int check_generic_dims(mpcq_ctx *c)
+{
+    int rc = check_ctx(c, kNone);
+    if (rc) return rc;
+    if (c->mimo_only) return fail(MPCQ_ERR_ARG, "n > 32 or m > 64 per plant: this context is served by mpcq_mimo_* only");
     return MPCQ_OK;
 }
 
@@ -372,7 +399,8 @@ int mpcq_destroy(mpcq_ctx *c)
                     c->d_setup_status, c->d_q, c->d_u, c->d_l, c->d_x, c->d_y, c->d_rho, c->d_status, c->d_iter,
                     c->d_xs, c->d_zs, c->d_ys, c->d_rhos, c->d_snx, c->d_sny, c->d_Fx, c->d_Fu, c->d_Fr,
                     c->d_Sbar, c->d_Ku, c->d_W0, c->d_X, c->d_U, c->d_img, c->d_list, c->d_counts,
-                    c->d_itstate, c->d_Ad, c->d_Bd, c->d_step, c->d_flags, c->d_stamps, c->d_mimo, c->d_sched, c->d_qlist};
+                    c->d_itstate, c->d_Ad, c->d_Bd, c->d_step, c->d_flags, c->d_stamps, c->d_mimo, c->d_sched, c->d_qlist,
+                    c->d_it_acc, c->d_uns_acc};
     if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
     if (c->graph) (void)hipGraphDestroy(c->graph);
     for (void *p : ptrs)
@@ -470,14 +498,13 @@ int setup_on_device(mpcq_ctx *c, hipStream_t s)
 int mpcq_setup(mpcq_ctx *c, const double *P, const double *q0, const double *A, const double *l0,
                const double *u0)
 {
-    int rc = check_ctx(c, false);
+    int rc = check_generic_dims(c);
     if (rc) return rc;
-    if (c->mimo_only) return fail(MPCQ_ERR_ARG, "n > 32 per-plant contexts are served by mpcq_mimo_* only");
     const size_t Pn = c->dims.n_plants, n = c->dims.n, m = c->dims.m;
     if (!P || !q0 || (m && (!A || !l0 || !u0))) return fail(MPCQ_ERR_ARG, "null setup array");
     for (size_t i = 0; i < Pn * m; i++)
         if (l0[i] > u0[i]) return fail(MPCQ_ERR_BOUNDS, "lower bound above upper bound (osqp validate_data)");
-    c->setup_done = false;
+    c->mode = mpcq_ctx::Mode::None;
     // rows n + j of A are the negated rows j (the reference's Gbar = [K0 L; -K0 L],
     // ModelPredictiveControlAPI.cpp:332-347), checked bit for bit: the tile kernel's paired loop
     c->paired = Pn == 1 && m == 2 * n && n % 4 == 0;
@@ -491,13 +518,13 @@ int mpcq_setup(mpcq_ctx *c, const double *P, const double *q0, const double *A, 
     if ((rc = setup_on_device(c, s))) return rc;
     c->lower_free = lower_all_free(c, l0);
     c->gen++;
-    c->setup_done = true;
+    c->mode = mpcq_ctx::Mode::Generic;
     return MPCQ_OK;
 }
 
 int mpcq_update_lin_cost(mpcq_ctx *c, const double *q)
 {
-    int rc = check_ctx(c, true);
+    int rc = check_ctx(c, kGeneric);
     if (rc) return rc;
     if (!q) return fail(MPCQ_ERR_ARG, "null q");
     return h2d(c->d_q, q, 8 * (size_t)c->dims.batch * c->dims.n, c->last);
@@ -505,7 +532,7 @@ int mpcq_update_lin_cost(mpcq_ctx *c, const double *q)
 
 int mpcq_update_upper_bound(mpcq_ctx *c, const double *u)
 {
-    int rc = check_ctx(c, true);
+    int rc = check_ctx(c, kGeneric);
     if (rc) return rc;
     if (!u) return fail(MPCQ_ERR_ARG, "null u");
     return h2d(c->d_u, u, 8 * (size_t)c->dims.batch * c->dims.m, c->last);
@@ -513,7 +540,7 @@ int mpcq_update_upper_bound(mpcq_ctx *c, const double *u)
 
 int mpcq_update_lower_bound(mpcq_ctx *c, const double *l)
 {
-    int rc = check_ctx(c, true);
+    int rc = check_ctx(c, kGeneric);
     if (rc) return rc;
     if (!l) return fail(MPCQ_ERR_ARG, "null l");
     const bool lf = lower_all_free_batch(c, l);
@@ -530,7 +557,7 @@ int mpcq_update_bounds(mpcq_ctx *c, const double *l, const double *u)
 
 int mpcq_cold_start(mpcq_ctx *c)
 {
-    int rc = check_ctx(c, true);
+    int rc = check_ctx(c, kGeneric);
     if (rc) return rc;
     if ((rc = reset_state(c, false))) return rc;
     HIPCHK(hipStreamSynchronize(c->last));
@@ -539,7 +566,7 @@ int mpcq_cold_start(mpcq_ctx *c)
 
 int mpcq_warm_start(mpcq_ctx *c, const double *x, const double *y)
 {
-    int rc = check_ctx(c, true);
+    int rc = check_ctx(c, kGeneric);
     if (rc) return rc;
     if (!x || (c->dims.m && !y)) return fail(MPCQ_ERR_ARG, "null x/y");
     // stage in the output buffers (overwritten by the next solve)
@@ -726,32 +753,46 @@ static int launch_queue(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s)
     return 0;
 }
 
+// The device path of this context's next solve, decided in one place for launch_args and
+// mpcq_get_path: per-plant contexts run one QP per wave (n <= 32, m <= 64) or one QP per lane;
+// shared-plant contexts run the MFMA tile kernel's phase chain (its tail one QP per wave), except
+// that small batches (under 512 tile waves: latency-bound) run one QP per wave throughout.
+struct PathChoice {
+    int kind;    // MPCQ_PATH_*
+    bool paired; // the tile kernel's paired loop
+};
+static PathChoice choose_path(const mpcq_ctx *c)
+{
+    const char *k = env_kernel();
+    const bool fits_wave = c->dims.n <= 32 && c->dims.m <= 64;
+    PathChoice p{MPCQ_PATH_LANE, false};
+    if (std::strcmp(k, "lane") == 0 || !fits_wave) return p;
+    if (!c->tile) return {MPCQ_PATH_WAVE, false};
+    const bool small = c->dims.batch < 8192 && std::strcmp(k, "tile") != 0;
+    if (small || std::strcmp(k, "wave") == 0) return {MPCQ_PATH_WAVE, false};
+    return {MPCQ_PATH_TILE, c->paired && c->all_ineq && c->lower_free};
+}
+
 template <typename T>
 static int launch_args(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s)
 {
-    const int B = c->dims.batch;
-    if (!c->tile) {
-        // per-plant batches: one QP per wave (operators in VGPRs); the lane kernel for shapes the wave
-        // kernel does not compile (n > 32 or m > 64) or when forced by the test hook
-        if (std::strcmp(env_kernel(), "lane") != 0 && c->dims.n <= 32 && c->dims.m <= 64) {
-            a.stop_iter = c->set.max_iter;
-            return wave_launch<T>(c, a, B, s);
-        }
+    const PathChoice p = choose_path(c);
+    a.paired = p.paired;
+    if (p.kind == MPCQ_PATH_LANE)
         return std::is_same<T, float>::value
                    ? mpcq_internal_admm_launch_f32((const mpcq::AdmmArgs<float> *)&a, c->nc, c->mc, s)
                    : mpcq_internal_admm_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->nc, c->mc, s);
+    if (!c->tile) {  // per-plant batches: one QP per wave (operators in VGPRs)
+        a.stop_iter = c->set.max_iter;
+        return wave_launch<T>(c, a, c->dims.batch, s);
     }
-    // phases whose QPs are few (the slow tail) run one QP per wave
-    const bool all_wave = std::strcmp(env_kernel(), "wave") == 0;
-    // Small batches (under 512 tile waves) are latency-bound: one QP per wave from the start.
-    const bool small = B < 8192 && std::strcmp(env_kernel(), "tile") != 0;
     const char *sch = std::getenv("MPCQ_TILE_SCHED");
     c->wq_last = false;
-    if (sch && std::strcmp(sch, "queue") == 0 && !all_wave && !small) {
+    if (p.kind == MPCQ_PATH_TILE && sch && std::strcmp(sch, "queue") == 0) {
         c->wq_last = true;
         return launch_queue<T>(c, a, s);
     }
-    return launch_phases<T>(c, a, s, all_wave || small);
+    return launch_phases<T>(c, a, s, p.kind == MPCQ_PATH_WAVE);
 }
 
 template <typename T>
@@ -780,7 +821,7 @@ static int launch_solve(mpcq_ctx *c, hipStream_t s, bool mpc, const double *X, d
 
 int mpcq_reset(mpcq_ctx *c)
 {
-    int rc = check_ctx(c, true);
+    int rc = check_ctx(c, kAnySetup);
     if (rc) return rc;
     c->fresh = true;
     return MPCQ_OK;
@@ -788,9 +829,8 @@ int mpcq_reset(mpcq_ctx *c)
 
 int mpcq_solve(mpcq_ctx *c, void *stream)
 {
-    int rc = check_ctx(c, true);
+    int rc = check_ctx(c, kGeneric);
     if (rc) return rc;
-    if (c->mimo_only) return fail(MPCQ_ERR_ARG, "n > 32 per-plant contexts are served by mpcq_mimo_* only");
     return launch_solve(c, (hipStream_t)stream, false, nullptr, nullptr, 0.0);
 }
 
@@ -804,7 +844,7 @@ static int d2h(mpcq_ctx *c, void *dst, const void *src, size_t bytes)
 
 int mpcq_get_solution(mpcq_ctx *c, double *x)
 {
-    int rc = check_ctx(c, true);
+    int rc = check_ctx(c, kAnySetup);
     if (rc) return rc;
     if (!x) return fail(MPCQ_ERR_ARG, "null x");
     return d2h(c, x, c->d_x, 8 * (size_t)c->dims.batch * c->dims.n);
@@ -812,7 +852,7 @@ int mpcq_get_solution(mpcq_ctx *c, double *x)
 
 int mpcq_get_dual(mpcq_ctx *c, double *y)
 {
-    int rc = check_ctx(c, true);
+    int rc = check_ctx(c, kAnySetup);
     if (rc) return rc;
     if (!y && c->dims.m) return fail(MPCQ_ERR_ARG, "null y");
     return d2h(c, y, c->d_y, 8 * (size_t)c->dims.batch * c->dims.m);
@@ -820,7 +860,7 @@ int mpcq_get_dual(mpcq_ctx *c, double *y)
 
 int mpcq_get_info(mpcq_ctx *c, int *status, int *iter, double *rho)
 {
-    int rc = check_ctx(c, true);
+    int rc = check_ctx(c, kAnySetup);
     if (rc) return rc;
     const size_t B = c->dims.batch;
     if (c->d_sched && c->wq_last) {  // the tile work queue flags a wave that polled past its limit (never expected)
@@ -835,7 +875,7 @@ int mpcq_get_info(mpcq_ctx *c, int *status, int *iter, double *rho)
 
 int mpcq_get_scaling(mpcq_ctx *c, double *D, double *E, double *cc)
 {
-    int rc = check_ctx(c, true);
+    int rc = check_ctx(c, kGeneric);
     if (rc) return rc;
     if (D) std::copy(c->hD.begin(), c->hD.end(), D);
     if (E) std::copy(c->hE.begin(), c->hE.end(), E);
@@ -846,15 +886,9 @@ int mpcq_get_scaling(mpcq_ctx *c, double *D, double *E, double *cc)
 int mpcq_get_path(mpcq_ctx *c, int *kind, int *paired)
 {
     if (!c) return fail(MPCQ_ERR_ARG, "null context");
-    const char *k = env_kernel();
-    int kd;
-    if (c->tile && std::strcmp(k, "lane") != 0) kd = std::strcmp(k, "wave") == 0 ? MPCQ_PATH_WAVE : MPCQ_PATH_TILE;
-    else kd = (std::strcmp(k, "lane") == 0 || c->dims.n > 32 || c->dims.m > 64) ? MPCQ_PATH_LANE : MPCQ_PATH_WAVE;
-    if (kind) *kind = kd;
-    if (paired) {
-        const char *pe = std::getenv("MPCQ_PAIRED");
-        *paired = kd == MPCQ_PATH_TILE && c->paired && c->all_ineq && c->lower_free && !(pe && !std::strcmp(pe, "0"));
-    }
+    const PathChoice p = choose_path(c);
+    if (kind) *kind = p.kind;
+    if (paired) *paired = p.paired;
     return MPCQ_OK;
 }
 
@@ -893,7 +927,7 @@ bool alloc_mpc_ops(mpcq_ctx *c, int nx)
 int mpcq_mpc_set_operators(mpcq_ctx *c, int nx, const double *Fx, const double *Fu, const double *Fr,
                            const double *Sbar, const double *Ku, const double *W0)
 {
-    int rc = check_ctx(c, false);
+    int rc = check_generic_dims(c);
     if (rc) return rc;
     const size_t Pn = c->dims.n_plants, n = c->dims.n, m = c->dims.m;
     if (nx <= 0 || nx > 8) return fail(MPCQ_ERR_ARG, "nx must be in 1..8");
@@ -912,7 +946,7 @@ int mpcq_mpc_set_operators(mpcq_ctx *c, int nx, const double *Fx, const double *
 
 int mpcq_mpc_step_device(mpcq_ctx *c, const double *X, double *U, double xref, void *stream)
 {
-    int rc = check_ctx(c, true);
+    int rc = check_ctx(c, kGeneric);
     if (rc) return rc;
     if (!c->mpc_ready) return fail(MPCQ_ERR_ORDER, "mpcq_mpc_set_operators has not been called");
     if (!X || !U) return fail(MPCQ_ERR_ARG, "null X/U");
@@ -921,7 +955,7 @@ int mpcq_mpc_step_device(mpcq_ctx *c, const double *X, double *U, double xref, v
 
 int mpcq_mpc_step(mpcq_ctx *c, const double *X, double *U, double xref)
 {
-    int rc = check_ctx(c, true);
+    int rc = check_ctx(c, kGeneric);
     if (rc) return rc;
     if (!c->mpc_ready) return fail(MPCQ_ERR_ORDER, "mpcq_mpc_set_operators has not been called");
     const size_t B = c->dims.batch;
@@ -932,7 +966,7 @@ int mpcq_mpc_step(mpcq_ctx *c, const double *X, double *U, double xref)
 
 int mpcq_mpc_set_plant(mpcq_ctx *c, int nx, const double *Ad, const double *Bd)
 {
-    int rc = check_ctx(c, false);
+    int rc = check_generic_dims(c);
     if (rc) return rc;
     if (nx <= 0 || nx > 8 || !Ad || !Bd) return fail(MPCQ_ERR_ARG, "set_plant: 1 <= nx <= 8 and Ad, Bd required");
     const size_t Pn = c->dims.n_plants;
@@ -941,19 +975,32 @@ int mpcq_mpc_set_plant(mpcq_ctx *c, int nx, const double *Ad, const double *Bd)
         for (double **p : {&c->d_Ad, &c->d_Bd})
             if (*p) { (void)hipFree(*p); *p = nullptr; }
     }
+    if (!c->d_it_acc) c->gen++;  // (the counters are baked into captured graphs)
     if ((!c->d_Ad && hipMalloc((void **)&c->d_Ad, 8 * Pn * nx * nx) != hipSuccess) ||
         (!c->d_Bd && hipMalloc((void **)&c->d_Bd, 8 * Pn * nx) != hipSuccess) ||
-        (!c->d_step && hipMalloc((void **)&c->d_step, 8) != hipSuccess))
+        (!c->d_step && hipMalloc((void **)&c->d_step, 8) != hipSuccess) ||
+        (!c->d_it_acc && hipMalloc((void **)&c->d_it_acc, 4 * (size_t)c->dims.batch) != hipSuccess) ||
+        (!c->d_uns_acc && hipMalloc((void **)&c->d_uns_acc, 4 * (size_t)c->dims.batch) != hipSuccess))
         return fail(MPCQ_ERR_HIP, "hipMalloc failed");
     c->plant_nx = nx;
     if ((rc = h2d(c->d_Ad, Ad, 8 * Pn * nx * nx, c->last)) || (rc = h2d(c->d_Bd, Bd, 8 * Pn * nx, c->last))) return rc;
     return MPCQ_OK;
 }
 
+int mpcq_mpc_stream_counters(mpcq_ctx *c, int *iters, int *unsolved)
+{
+    int rc = check_ctx(c, kGeneric);
+    if (rc) return rc;
+    if (!c->d_it_acc) return fail(MPCQ_ERR_ORDER, "mpcq_mpc_set_plant has not been called");
+    const size_t B = c->dims.batch;
+    if ((rc = d2h(c, iters, c->d_it_acc, 4 * B))) return rc;
+    return d2h(c, unsolved, c->d_uns_acc, 4 * B);
+}
+
 int mpcq_mpc_simulate_device(mpcq_ctx *c, double *X, const double *U, unsigned long long seed, long long first_qp,
                              long long step, double noise_std, void *stream)
 {
-    int rc = check_ctx(c, false);
+    int rc = check_generic_dims(c);
     if (rc) return rc;
     if (!c->plant_nx) return fail(MPCQ_ERR_ORDER, "mpcq_mpc_set_plant has not been called");
     if (!X || !U) return fail(MPCQ_ERR_ARG, "null X/U");
@@ -967,14 +1014,21 @@ int mpcq_mpc_simulate_device(mpcq_ctx *c, double *X, const double *U, unsigned l
 int mpcq_mpc_run_device(mpcq_ctx *c, double *X, double *U, double xref, int steps, unsigned long long seed,
                         long long first_qp, long long first_step, double noise_std, void *stream)
 {
-    int rc = check_ctx(c, true);
+    int rc = check_ctx(c, kGeneric);
     if (rc) return rc;
     if (!c->mpc_ready || !c->plant_nx) return fail(MPCQ_ERR_ORDER, "mpc operators / plant not set");
     if (c->plant_nx != c->nx) return fail(MPCQ_ERR_ARG, "plant nx differs from the operators' nx");
     if (!X || !U || steps < 0) return fail(MPCQ_ERR_ARG, "null X/U or steps < 0");
     if (!stream) return fail(MPCQ_ERR_ARG, "graph capture needs a non-NULL stream");
     hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipMemsetAsync(c->d_it_acc, 0, 4 * (size_t)c->dims.batch, s));
+    HIPCHK(hipMemsetAsync(c->d_uns_acc, 0, 4 * (size_t)c->dims.batch, s));
     if (steps == 0) return MPCQ_OK;
+    struct Acc {  // this call's launches (eager and captured) accumulate the stream counters
+        mpcq_ctx *c;
+        explicit Acc(mpcq_ctx *cc) : c(cc) { c->stream_acc = true; }
+        ~Acc() { c->stream_acc = false; }
+    } acc(c);
     if (mpcq_internal_set_step(c->d_step, first_step, s)) return fail(MPCQ_ERR_HIP, "set_step launch failed");
     const char *dbg = std::getenv("MPCQ_DEBUG_SYNC");  // debugging hook: synchronise every stage
     const bool sync_each = dbg && dbg[0] == '1';
@@ -1008,10 +1062,17 @@ int mpcq_mpc_run_device(mpcq_ctx *c, double *X, double *U, double xref, int step
             lrc = fail(MPCQ_ERR_HIP, "simulate kernel launch failed");
         hipGraph_t g = nullptr;
         const hipError_t ec = hipStreamEndCapture(s, &g);
+        // a discarded capture ran none of its launches: the phase-list counters are not known clean
+        if (lrc || ec != hipSuccess) c->count0_clean = false;
         if (lrc) { if (g) (void)hipGraphDestroy(g); return lrc; }
         if (ec != hipSuccess) return fail(MPCQ_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ec));
         c->graph = g;
-        HIPCHK(hipGraphInstantiate(&c->gexec, c->graph, nullptr, nullptr, 0));
+        const hipError_t ei = hipGraphInstantiate(&c->gexec, c->graph, nullptr, nullptr, 0);
+        if (ei != hipSuccess) {
+            c->count0_clean = false;
+            c->gexec = nullptr;
+            return fail(MPCQ_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
+        }
         c->gkey = {X, U, xref, noise_std, seed, first_qp, s, c->gen};
     }
     for (int k = done; k < steps; k++) {
@@ -1083,7 +1144,7 @@ int mpcq_mpc_setup_plants_device(mpcq_ctx *c, int nx, int s_rows, const double *
                                  const double *Cd, const double *K, const double *Q, const double *R,
                                  const double *RD, void *stream)
 {
-    int rc = check_ctx(c, false);
+    int rc = check_generic_dims(c);
     if (rc) return rc;
     const size_t Pn = c->dims.n_plants, n = c->dims.n, m = c->dims.m;
     if (nx <= 0 || nx > 8 || s_rows < 0) return fail(MPCQ_ERR_ARG, "setup_plants: 1 <= nx <= 8, s_rows >= 0");
@@ -1091,7 +1152,7 @@ int mpcq_mpc_setup_plants_device(mpcq_ctx *c, int nx, int s_rows, const double *
     if (!Ad || !Bd || !Cd || !K || !Q || !R || !RD) return fail(MPCQ_ERR_ARG, "setup_plants: null plant array");
     if (!alloc_mpc_ops(c, nx)) return fail(MPCQ_ERR_HIP, "hipMalloc failed");
     c->nx = nx;
-    c->setup_done = false;
+    c->mode = mpcq_ctx::Mode::None;
     hipStream_t s = (hipStream_t)stream;
     c->last = s;
     mpcq::CondenseArgs a{};
@@ -1115,7 +1176,7 @@ int mpcq_mpc_setup_plants_device(mpcq_ctx *c, int nx, int s_rows, const double *
     c->lower_free = true;  // l0 = -DBL_MAX on every row (:42)
     c->gen++;
     c->mpc_ready = true;
-    c->setup_done = true;
+    c->mode = mpcq_ctx::Mode::Generic;
     return MPCQ_OK;
 }
 
@@ -1124,7 +1185,7 @@ int mpcq_mimo_setup_plants_device(mpcq_ctx *c, int nx, int nu, int ny, int s_row
                                   const double *Cd, const double *Q, const double *R, const double *RD, const double *K,
                                   const double *K0, const double *w0, void *stream)
 {
-    int rc = check_ctx(c, false);
+    int rc = check_ctx(c, kNone);
     if (rc) return rc;
     const int n = c->dims.n, m = c->dims.m;
     if (nu != 1 && nu != 2 && nu != 4) return fail(MPCQ_ERR_ARG, "mimo: n_u must be 1, 2 or 4");
@@ -1142,7 +1203,7 @@ int mpcq_mimo_setup_plants_device(mpcq_ctx *c, int nx, int nu, int ny, int s_row
     if (!c->d_mimo && hipMalloc((void **)&c->d_mimo, 8 * (size_t)L.total * c->dims.n_plants) != hipSuccess)
         return fail(MPCQ_ERR_HIP, "hipMalloc failed (mimo operator blocks)");
     c->mimo_N = N; c->mimo_nx = nx; c->mimo_nu = nu; c->mimo_ny = ny; c->mimo_srows = s_rows;
-    c->mimo_ready = false;
+    c->mode = mpcq_ctx::Mode::None;
     c->gen++;
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipMemsetAsync(c->d_flags, 0, 4, s));
@@ -1177,20 +1238,21 @@ int mpcq_mimo_setup_plants_device(mpcq_ctx *c, int nx, int nu, int ny, int s_row
             std::fclose(f);
         }
     }
+    if (flags & 1) return fail(MPCQ_ERR_SETUP, "mimo: P + sigma I is not positive definite (non-convex QP)");
     if (flags & 2) return fail(MPCQ_ERR_SETUP, "mimo: a constraint row is not an inequality (|w0| beyond OSQP_INFTY)");
     c->mimo_diag_k0 = (flags & 4) ? 0 : 1;
     c->last = s;
     c->fresh = true;  // the first step starts from x = z = y = 0, rho = settings.rho (initSolver, :64)
-    c->mimo_ready = true;
-    c->setup_done = true;
+    c->mpc_ready = false;  // the generic front-end operators no longer describe this context
+    c->mode = mpcq_ctx::Mode::Mimo;
     return MPCQ_OK;
 }
 
 int mpcq_mimo_step_device(mpcq_ctx *c, const double *X, double *U, const double *yref, void *stream)
 {
-    int rc = check_ctx(c, false);
+    int rc = check_ctx(c, kNone);
     if (rc) return rc;
-    if (!c->mimo_ready) return fail(MPCQ_ERR_ORDER, "mpcq_mimo_setup_plants_device has not succeeded");
+    if (c->mode != mpcq_ctx::Mode::Mimo) return fail(MPCQ_ERR_ORDER, "mpcq_mimo_setup_plants_device has not succeeded");
     if (!X || !U) return fail(MPCQ_ERR_ARG, "null X/U");
     mpcq::MimoArgs a{};
     a.batch = c->dims.batch;

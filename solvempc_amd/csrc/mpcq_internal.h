@@ -164,6 +164,9 @@ struct AdmmArgs {
     // outputs
     double *x, *y, *rho_out;
     int *status, *iter;
+    // receding-horizon stream counters (mpcq_mpc_run_device; null otherwise): per QP, the iterations of
+    // every solve and the solves that did not end SOLVED, accumulated at finalize
+    int *it_acc, *uns_acc;
     // MPC front end (n = N, m = 2N); null when unused
     int mpc, nx;
     const double *X, *Fx, *Fu, *Fr, *Sbar, *Ku, *W0;

@@ -695,6 +695,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 a.status[b] = sta;
                 a.iter[b] = it;
                 a.rho_out[b] = (double)rho[gi];
+                if (a.it_acc) {
+                    a.it_acc[b] += it;
+                    a.uns_acc[b] += sta != kSolved;
+                }
             }
         }
     };

@@ -238,6 +238,10 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
             a.status[b] = status;
             a.iter[b] = it;
             a.rho_out[b] = (double)rho;
+            if (a.it_acc) {
+                a.it_acc[b] += it;
+                a.uns_acc[b] += status != kSolved;
+            }
         }
     };
     if (status != kUnsolved) {

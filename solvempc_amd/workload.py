@@ -66,6 +66,22 @@ def mpc_states(seed: int, start: int, count: int, u_range: float = 1.0):
     return X, U
 
 
+# Config 5 (receding-horizon stream) starts inside the reference controller's region of attraction.
+# The config-2 law above puts |K X| ~ 1,200 on the inner loop's PWM command (K = [-50, -150, 5500,
+# 350], K X = -(PWM) + K0 U with |PWM| <= 255 the constraint rows of ModelPredictiveControlAPI.cpp:
+# 335,364-368): the actuator saturates from the first step and the cart-pole's open-loop pole
+# (|lambda| = 1.0797 in Ad + Bd K / K0) diverges whatever the QP returns (measured with the oracle:
+# x1.08 per step).  A tenth of that spread (|K X| ~ 120) with the reference's own initial input
+# U = 0 (:23) keeps every plant SOLVED and bounded over 1,000 steps at noise std 1e-2.
+STREAM_X_SCALE = 0.1
+
+
+def stream_states(seed: int, start: int, count: int):
+    """Config 5 initial states: X ~ N(0, STREAM_X_SCALE^2 diag(.1,.1,.05,.5)), U = 0."""
+    X = normals(seed, start, count, 4) * (X_STD * STREAM_X_SCALE)
+    return X, np.zeros(count)
+
+
 def randomized_plants(plant: dict, seed: int, start: int, count: int, rel: float = 0.02, attempts: int = 64):
     """Config 3 plants for global indices start .. start+count-1: Ad = Ad0 o (1 + rel eps),
     Bd = Bd0 o (1 + rel eps), eps ~ N(0, 1) (Box-Muller on draws 32a .. 32a+19 of attempt a); a draw
@@ -121,14 +137,31 @@ def flops_per_qp(n: int, m: int, nx: int, iters: np.ndarray, check: int = 25, pa
     """Algorithmic FLOPs of one solve: iters*F_iter + checks*F_check + front end.
     F_iter = 4nm + 2n^2 + 9m + 6n; F_check = 4nm + 2n^2 + 6m + 4n; front end (q, u, W'q^)
     = 2n(nx+1+n) + 2m(nx+1) + 2n^2.  No refactorisation FLOPs: rho updates are diagonal.
-    paired: the tile kernel's paired loop (rows n + j of A = -rows j) performs B'w and B eta over
-    m/2 rows, F_iter = 2nm + 2n^2 + 9m + 6n (the reduced count it actually performs; SURVEY §8d asks
-    for it when the A structure is exploited); its check iterations keep the dense F_check."""
+    paired: the tile kernel's paired loop (rows n + j of A = -rows j) performs every A product (B'w,
+    B eta, and A x, A'y of the check iterations) over the m/2 distinct rows: F_iter = 2nm + 2n^2 +
+    9m + 6n, F_check = 2nm + 2n^2 + 6m + 4n (the reduced counts it performs; SURVEY §8d asks for
+    them when the A structure is exploited)."""
     it = np.asarray(iters, dtype=np.float64)
-    f_iter = (2 if paired else 4) * n * m + 2 * n * n + 9 * m + 6 * n
-    f_check = 4 * n * m + 2 * n * n + 6 * m + 4 * n
-    f_front = 2 * n * (nx + 1 + n) + 2 * m * (nx + 1) + 2 * n * n
+    f_iter, f_check, f_front = _flop_terms(n, m, nx, paired)
     return it * f_iter + np.floor(it / check) * f_check + f_front
+
+
+def _flop_terms(n: int, m: int, nx: int, paired: bool):
+    rows = m // 2 if paired else m  # the paired loop's A products run over the m/2 distinct rows
+    f_iter = 4 * n * rows + 2 * n * n + 9 * m + 6 * n
+    f_check = 4 * n * rows + 2 * n * n + 6 * m + 4 * n
+    f_front = 2 * n * (nx + 1 + n) + 2 * m * (nx + 1) + 2 * n * n
+    return f_iter, f_check, f_front
+
+
+def flops_per_qp_total(n: int, m: int, nx: int, iters_total, solves: int, check: int = 25,
+                       paired: bool = False) -> np.ndarray:
+    """flops_per_qp over `solves` warm-started solves of each QP from the device's per-QP total of
+    iterations (mpcq_mpc_stream_counters); checks counted as floor(total / check) (every solve of
+    the stream stops on a check iteration, so this is exact when none hits max_iter)."""
+    it = np.asarray(iters_total, dtype=np.float64)
+    f_iter, f_check, f_front = _flop_terms(n, m, nx, paired)
+    return it * f_iter + np.floor(it / check) * f_check + solves * f_front
 
 
 def flops_plant_setup(n: int, m: int, N: int | None = None) -> float:

@@ -66,3 +66,25 @@ def test_blocks_tile_the_stream():
     # counter-based states are shard-invariant
     a = np.concatenate([workload.mpc_states(1, s, c)[0] for s, c in (mdist.strong_block(100, r, 4) for r in range(4))])
     np.testing.assert_array_equal(a, workload.mpc_states(1, 0, 100)[0])
+
+
+def test_bench_launches_its_own_ranks():
+    """`python bench.py --gpus 2` spawns its two ranks itself (RANK / WORLD_SIZE / MASTER_* per child,
+    before any device call); the dry run does the rendezvous and the per-step gather over gloo and
+    rank 0 prints the one JSON line with the world size the gather saw."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2", "--backend", "gloo", "--dry-run",
+                        "--steps", "3", "--warmup", "1", "--batch", "1000"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["steps"] == 3 and rec["dry_run"] is True
+    assert rec["collective"] == {"backend": "gloo", "world_size": 2, "gathered": 2000, "matches_stream": True}

@@ -179,3 +179,28 @@ def test_quadrotor_plants_and_oracle_solve():
     Un, x, st, it = oracle.mimo_plants_step(workload.quadrotor_shared(), Ad, Bd, X, U, 30, nthreads=4)
     assert np.all(st == oracle.SOLVED)
     assert np.all(np.abs(Un) <= np.array(workload.QUAD["w0"]) + 1e-3)  # the applied input stays in the box
+
+
+def test_stream_workload_closed_loop_is_bounded():
+    """Config 5's initial-state law (workload.stream_states) keeps the reference controller's closed
+    loop (oracle controllerStep + X <- Ad X + Bd U + w, noise std 1e-2) SOLVED and bounded, where the
+    config-2 law saturates the inner loop and diverges (workload.STREAM_X_SCALE)."""
+    from solvempc_amd import workload
+
+    plant = workload.reference_plant()
+    N, B, steps = 20, 8, 300
+    ops = oracle.condense(plant, N)
+    l = np.full(2 * N, -np.finfo(np.float64).max)
+    for law, bounded in (("stream", True), ("cfg2", False)):
+        X, U = workload.stream_states(4, 0, B) if law == "stream" else workload.mpc_states(4, 0, B)
+        rs = [oracle.Solver(ops["P"], np.zeros(N), ops["A"], l, ops["W0"]) for _ in range(B)]
+        for k in range(steps):
+            for b, r in enumerate(rs):
+                assert r.update_gradient(oracle.gradient(ops, X[b], U[b]))
+                assert r.update_upper_bound(oracle.upper_bound(ops, X[b], U[b]))
+                if r.solve() == oracle.SOLVED:
+                    U[b] += r.x()[0]
+                else:
+                    assert not bounded
+            X = workload.simulate(plant["Ad"], plant["Bd"], X, U, workload.plant_noise(4, 0, B, k, 4, 1e-2))
+        assert (np.abs(X).max() < 10) == bounded, (law, np.abs(X).max())
