@@ -45,7 +45,6 @@ __device__ bool primal_infeasible(const AdmmArgs<T> &a, const PlantOps<T> &op, c
                                   const T *lh, int b, T eps, bool scaled)
 {
     // lh == nullptr: every lower bound is -inf (LFREE kernel variant)
-    const size_t B = a.batch;
     auto dyj = [&](int j) -> T {  // delta_y projected onto the polar of the recession cone of [l,u]
         T d = a.ys[b * MC + j] - a.snap_y[b * MC + j];
         const T up = uh[j * 64], lo = lh ? lh[j * 64] : T(-kInfty);
@@ -80,7 +79,6 @@ template <typename T, int NC, int MC>
 __device__ bool dual_infeasible(const AdmmArgs<T> &a, const PlantOps<T> &op, const T *g,
                                 const T *uh, const T *lh, int b, T eps, bool scaled)
 {
-    const size_t B = a.batch;
     auto dxp = [&](int k) -> T { return a.xs[b * NC + k] - a.snap_x[b * NC + k]; };
     T qdx = 0;  // q^' dx^ = (W' q^)' dx'
 #pragma unroll 1
@@ -160,7 +158,6 @@ void admm_lane_kernel(AdmmArgs<T> a)
     const int b = blockIdx.x * 64 + lane;
     if (b >= a.batch) return;  // lanes never exchange data: no barrier below
     const int n = a.n, m = a.m;
-    const size_t B = a.batch;
     const T *base0 = a.ops.lam + (SHARED ? 0 : (size_t)b * a.ops_stride);  // lam starts the block
     PlantOps<T> op;  // plain pointer view for the cold paths
     op.lam = base0 + L.lam; op.W = base0 + L.W; op.sWtW = base0 + L.sWtW; op.WtA = base0 + L.WtA;

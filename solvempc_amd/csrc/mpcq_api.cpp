@@ -36,6 +36,31 @@ int fail(int code, const std::string &msg)
 
 constexpr int kMaxPhases = 16;
 
+// Test hooks: the library reads exactly these environment variables, here and nowhere else.  Each
+// selects among production code paths so that the tests can cover every path on one device:
+//   MPCQ_KERNEL=lane|wave|tile  the ADMM kernel family (mpcq_get_path reports the choice)
+//   MPCQ_PHASES=0|k1,k2,..      the tile path's phase stops, in check_termination multiples
+//   MPCQ_SETUP=ref              per-plant setup on the workgroup kernel (mpcq_setup.hip)
+//   MPCQ_CONDENSE=ref           condensing on the workgroup kernel (mpcq_condense.hip)
+//   MPCQ_MIMO_GENERAL_K0=1      the MIMO solve's general-K0 exchange path on a diagonal K0
+// Debug builds (-DMPCQ_DEBUG_HOOKS) add the stamp / profiling dumps (MPCQ_TILE_STAMPS,
+// MPCQ_SETUP_PROF, MPCQ_MIMO_SETUP_STAMPS, MPCQ_MIMO_STAMPS) and MPCQ_DEBUG_SYNC.
+const char *test_hook(const char *name)
+{
+    const char *v = std::getenv(name);
+    return v ? v : "";
+}
+const char *debug_hook(const char *name)
+{
+#ifdef MPCQ_DEBUG_HOOKS
+    const char *v = std::getenv(name);
+    return v ? v : "";
+#else
+    (void)name;
+    return "";
+#endif
+}
+
 size_t setup_scratch_len(int n, int m)
 {
     return 7 * (size_t)n * n + (size_t)m * n + 3 * (size_t)n + 2 * (size_t)m + 64;
@@ -58,9 +83,6 @@ struct mpcq_ctx {
     int KN = 0, KM = 0;
     void *d_img = nullptr;
     int *d_list = nullptr, *d_counts = nullptr, *d_itstate = nullptr;
-    unsigned *d_sched = nullptr;  // tile work queue: TileSched counters
-    int *d_qlist = nullptr;       //                  [stage][batch] queue entries
-    bool wq_last = false;         // the last solve ran the work queue (its error word is valid)
     bool count0_clean = false;    // phase 0's ListSeg counters are zero (the last phase chain's final launch zeroed them)
     long long *d_stamps = nullptr;  // debug (MPCQ_TILE_STAMPS)
     hipStream_t last = nullptr;
@@ -302,9 +324,8 @@ int mpcq_create(const mpcq_dims *d, const mpcq_settings *s, mpcq_ctx **out)
         return fail(MPCQ_ERR_ARG, "invalid settings (osqp validate_settings)");
     int nc = 0, mc = 0;
     const int KN = (d->n + 3) / 4, KM = (std::max(d->m, 1) + 3) / 4;
-    const char *force = std::getenv("MPCQ_KERNEL");  // test hook: "lane" forces the per-lane kernel
     const bool tile = d->n_plants == 1 && mpcq_internal_tile_supported(KN, KM) &&
-                      !(force && std::strcmp(force, "lane") == 0);
+                      std::strcmp(test_hook("MPCQ_KERNEL"), "lane") != 0;
     if (tile) {
         nc = 16 * ((KN + 3) / 4);
         mc = 16 * ((KM + 3) / 4);
@@ -375,8 +396,6 @@ int mpcq_create(const mpcq_dims *d, const mpcq_settings *s, mpcq_ctx **out)
         A((void **)&c->d_list, 4 * 2 * lcap);
         A((void **)&c->d_counts, 4 * kMaxPhases * mpcq::ListSeg::kCounters);
         A((void **)&c->d_itstate, 4 * B);
-        A((void **)&c->d_sched, 4 * mpcq::TileSched::kWords);
-        A((void **)&c->d_qlist, 4 * (size_t)mpcq::kMaxStages * B);
     } else if (!c->mimo_only) {
         A(&c->d_snx, es * B * nc);
         A(&c->d_sny, es * B * mc);
@@ -399,7 +418,7 @@ int mpcq_destroy(mpcq_ctx *c)
                     c->d_setup_status, c->d_q, c->d_u, c->d_l, c->d_x, c->d_y, c->d_rho, c->d_status, c->d_iter,
                     c->d_xs, c->d_zs, c->d_ys, c->d_rhos, c->d_snx, c->d_sny, c->d_Fx, c->d_Fu, c->d_Fr,
                     c->d_Sbar, c->d_Ku, c->d_W0, c->d_X, c->d_U, c->d_img, c->d_list, c->d_counts,
-                    c->d_itstate, c->d_Ad, c->d_Bd, c->d_step, c->d_flags, c->d_stamps, c->d_mimo, c->d_sched, c->d_qlist,
+                    c->d_itstate, c->d_Ad, c->d_Bd, c->d_step, c->d_flags, c->d_stamps, c->d_mimo,
                     c->d_it_acc, c->d_uns_acc};
     if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
     if (c->graph) (void)hipGraphDestroy(c->graph);
@@ -440,17 +459,16 @@ int setup_on_device(mpcq_ctx *c, hipStream_t s)
     a.flags = c->d_flags;
     // one wavefront per plant, LDS-resident (mpcq_setup_wave.hip) where the plant fits; the
     // global-scratch workgroup kernel otherwise (MPCQ_SETUP=ref forces it: A/B test hook)
-    const char *se = std::getenv("MPCQ_SETUP");
-    const bool ref_setup = (se && !std::strcmp(se, "ref")) || !mpcq_internal_setup_wave_lds((int)n, (int)m);
+    const bool ref_setup = !std::strcmp(test_hook("MPCQ_SETUP"), "ref") || !mpcq_internal_setup_wave_lds((int)n, (int)m);
     if (ref_setup) {
         if (!c->d_scratch && hipMalloc((void **)&c->d_scratch, 8 * Pn * setup_scratch_len((int)n, (int)m)) != hipSuccess)
             return fail(MPCQ_ERR_HIP, "hipMalloc failed (setup scratch)");
         a.scratch = c->d_scratch;
         if (mpcq_internal_setup_launch(&a, s) != 0) return fail(MPCQ_ERR_HIP, "setup kernel launch failed");
     } else {
-        const char *pe = std::getenv("MPCQ_SETUP_PROF");  // debug hook: per-stage clock stamps to a file
+        const char *pe = debug_hook("MPCQ_SETUP_PROF");  // per-stage clock stamps to a file
         long long *prof = nullptr;
-        if (pe && *pe && hipMalloc((void **)&prof, 8 * 16 * Pn) == hipSuccess) {
+        if (*pe && hipMalloc((void **)&prof, 8 * 16 * Pn) == hipSuccess) {
             (void)hipMemsetAsync(prof, 0, 8 * 16 * Pn, s);
             a.prof = prof;
         }
@@ -588,17 +606,16 @@ int mpcq_warm_start(mpcq_ctx *c, const double *x, const double *y)
 
 // Phase boundaries of the tile path (multiples of check_termination, then max_iter): QPs still
 // running at a boundary are re-packed densely into the waves of the next launch.
-static int phase_stops(const mpcq_settings &st, int *stops, bool queue = false)
+static int phase_stops(const mpcq_settings &st, int *stops)
 {
     const int ct = st.check_termination;
     int np = 0;
-    const char *e = std::getenv("MPCQ_PHASES");  // test/benchmark hook: "0" = one launch per solve,
-                                                  // or a comma list of check multiples ("3,4,5,6,8")
+    const char *e = test_hook("MPCQ_PHASES");  // "0" = one launch per solve, or check multiples "3,4,5"
     int mult[kMaxPhases] = {3, 4, 5, 6, 8, 12, 20, 40, 80, 160};
-    int nm = queue ? 3 : 10;  // work queue: the few QPs past 5 checks finish in place (no more hand-offs)
-    const int cap = queue ? mpcq::kMaxStages : kMaxPhases;
-    if (e && e[0] == '0') nm = 0;
-    else if (e && *e) {
+    int nm = 10;
+    const int cap = kMaxPhases;
+    if (e[0] == '0') nm = 0;
+    else if (*e) {
         nm = 0;
         for (const char *p = e; *p && nm < cap - 1;) {
             mult[nm++] = std::atoi(p);
@@ -618,11 +635,7 @@ static int phase_stops(const mpcq_settings &st, int *stops, bool queue = false)
     return np;
 }
 
-static const char *env_kernel()
-{
-    const char *e = std::getenv("MPCQ_KERNEL");  // test hook: "lane", "wave" or "tile"
-    return e ? e : "";
-}
+static const char *env_kernel() { return test_hook("MPCQ_KERNEL"); }
 
 template <typename T>
 static int wave_launch(mpcq_ctx *c, const mpcq::AdmmArgs<T> &a, int grid, hipStream_t s)
@@ -649,13 +662,12 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
         return -2;
     c->count0_clean = false;
     const int mpc = a.mpc;
-    const char *te = std::getenv("MPCQ_TAIL_PHASE");
-    const int tail_from = wave_only ? 0 : (te ? std::atoi(te) : 3);
+    const int tail_from = wave_only ? 0 : 3;  // from the fourth launch on one QP per wave
     int np_run = 0;
     a.list_seg = seg;
 
-    // debug hook: per-wave stage stamps of every phase launch, written to $MPCQ_TILE_STAMPS after the solve
-    const char *stp = std::getenv("MPCQ_TILE_STAMPS");
+    // debug build: per-wave stage stamps of every phase launch, written to $MPCQ_TILE_STAMPS after the solve
+    const char *stp = debug_hook("MPCQ_TILE_STAMPS");
     const size_t waves = (size_t)(B + 15) / 16 + 4 * mpcq::ListSeg::kShards;
     if (stp && *stp && !c->d_stamps && hipMalloc((void **)&c->d_stamps, 8 * 8 * waves * kMaxPhases) != hipSuccess)
         return -2;
@@ -708,51 +720,6 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
     return 0;
 }
 
-// Experimental (MPCQ_TILE_SCHED=queue): the whole solve as one work-queue launch (mpcq_tile.h "Work
-// queue").  Correct, but slower than the phase chains on MI355X: its device-scope counter traffic
-// (~10 atomics per 16-QP group) serialises (measured 2.9 ms vs 0.47 ms per cfg2 solve).
-template <typename T>
-static int launch_queue(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s)
-{
-    const int B = c->dims.batch;
-    int qstops[kMaxPhases];
-    const int nq = phase_stops(c->set, qstops, true);
-    a.persistent = 1;
-    a.nstages = nq;
-    for (int k = 0; k < nq; k++) a.stops[k] = qstops[k];
-    a.sched = c->d_sched;
-    a.qlist = c->d_qlist;
-    a.it_state = c->d_itstate;
-    a.img = (const T *)c->d_img;
-    a.resume = 0;
-    a.stop_iter = qstops[nq - 1];
-    if (hipMemsetAsync(c->d_sched, 0, 4 * mpcq::TileSched::kWords, s) != hipSuccess) return -2;
-    if (nq > 1 && hipMemsetAsync(c->d_qlist + B, 0, 4 * (size_t)(nq - 1) * B, s) != hipSuccess) return -2;
-    const char *stp = std::getenv("MPCQ_TILE_STAMPS");
-    const size_t waves = (size_t)(B + 15) / 16 + 4;
-    if (stp && *stp && !c->d_stamps && hipMalloc((void **)&c->d_stamps, 8 * 8 * waves * kMaxPhases) != hipSuccess)
-        return -2;
-    if (stp && *stp && hipMemsetAsync(c->d_stamps, 0, 8 * 8 * waves, s) != hipSuccess) return -2;
-    a.stamps = (stp && *stp) ? c->d_stamps : nullptr;
-    const int rc = std::is_same<T, float>::value
-                       ? mpcq_internal_tile_launch_f32((const mpcq::AdmmArgs<float> *)&a, c->KN, c->KM, s)
-                       : mpcq_internal_tile_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->KN, c->KM, s);
-    if (rc) return rc;
-    if (stp && *stp) {
-        std::vector<long long> h(8 * waves);
-        if (hipMemcpyAsync(h.data(), c->d_stamps, 8 * h.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess)
-            return -2;
-        if (FILE *f = std::fopen(stp, "wb")) {
-            const long long hdr[2] = {1, (long long)waves};
-            std::fwrite(hdr, 8, 2, f);
-            std::fwrite(h.data(), 8, h.size(), f);
-            std::fclose(f);
-        }
-    }
-    return 0;
-}
-
 // The device path of this context's next solve, decided in one place for launch_args and
 // mpcq_get_path: per-plant contexts run one QP per wave (n <= 32, m <= 64) or one QP per lane;
 // shared-plant contexts run the MFMA tile kernel's phase chain (its tail one QP per wave), except
@@ -785,12 +752,6 @@ static int launch_args(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s)
     if (!c->tile) {  // per-plant batches: one QP per wave (operators in VGPRs)
         a.stop_iter = c->set.max_iter;
         return wave_launch<T>(c, a, c->dims.batch, s);
-    }
-    const char *sch = std::getenv("MPCQ_TILE_SCHED");
-    c->wq_last = false;
-    if (p.kind == MPCQ_PATH_TILE && sch && std::strcmp(sch, "queue") == 0) {
-        c->wq_last = true;
-        return launch_queue<T>(c, a, s);
     }
     return launch_phases<T>(c, a, s, p.kind == MPCQ_PATH_WAVE);
 }
@@ -863,11 +824,6 @@ int mpcq_get_info(mpcq_ctx *c, int *status, int *iter, double *rho)
     int rc = check_ctx(c, kAnySetup);
     if (rc) return rc;
     const size_t B = c->dims.batch;
-    if (c->d_sched && c->wq_last) {  // the tile work queue flags a wave that polled past its limit (never expected)
-        unsigned err = 0;
-        if ((rc = d2h(c, &err, c->d_sched + mpcq::TileSched::err(), 4))) return rc;
-        if (err) return fail(MPCQ_ERR_HIP, "tile work queue: a wave gave up polling (code " + std::to_string(err) + ")");
-    }
     if ((rc = d2h(c, status, c->d_status, 4 * B))) return rc;
     if ((rc = d2h(c, iter, c->d_iter, 4 * B))) return rc;
     return d2h(c, rho, c->d_rho, 8 * B);
@@ -1030,8 +986,7 @@ int mpcq_mpc_run_device(mpcq_ctx *c, double *X, double *U, double xref, int step
         ~Acc() { c->stream_acc = false; }
     } acc(c);
     if (mpcq_internal_set_step(c->d_step, first_step, s)) return fail(MPCQ_ERR_HIP, "set_step launch failed");
-    const char *dbg = std::getenv("MPCQ_DEBUG_SYNC");  // debugging hook: synchronise every stage
-    const bool sync_each = dbg && dbg[0] == '1';
+    const bool sync_each = debug_hook("MPCQ_DEBUG_SYNC")[0] == '1';  // synchronise every stage
     auto stage = [&](const char *what) -> int {
         if (!sync_each) return MPCQ_OK;
         const hipError_t e = hipStreamSynchronize(s);
@@ -1102,8 +1057,7 @@ int mpcq_condense(int device, int n_plants, int nx, int N, int s_rows, const dou
     const size_t Pn = n_plants, X = nx, n = N;
     const size_t in_cnt[] = {Pn * X * X, Pn * X, Pn * X, Pn * X, Pn, Pn, Pn};
     const size_t out_cnt[] = {Pn * n * n, Pn * 2 * n * n, Pn * n * X, Pn * n, Pn * n * n, Pn * 2 * n * X, Pn * 2 * n, Pn * 2 * n};
-    const char *ce = std::getenv("MPCQ_CONDENSE");  // test hook: "ref" forces the workgroup kernel
-    const bool force_ref = ce && !std::strcmp(ce, "ref");
+    const bool force_ref = !std::strcmp(test_hook("MPCQ_CONDENSE"), "ref");  // the workgroup kernel
     const size_t scr = (N > 32 || force_ref) ? Pn * mpcq_internal_condense_scratch(nx, N) : 0;
     size_t total = scr;
     for (size_t c : in_cnt) total += c;
@@ -1215,7 +1169,7 @@ int mpcq_mimo_setup_plants_device(mpcq_ctx *c, int nx, int nu, int ny, int s_row
     a.Ad = Ad; a.Bd = Bd; a.Cd = Cd; a.Q = Q; a.R = R; a.RD = RD; a.K = K; a.K0 = K0; a.w0 = w0;
     a.ops = c->d_mimo;
     a.flags = c->d_flags;
-    const char *sst = std::getenv("MPCQ_MIMO_SETUP_STAMPS");  // debug hook: per-plant phase stamps
+    const char *sst = debug_hook("MPCQ_MIMO_SETUP_STAMPS");  // per-plant phase stamps
     if (sst && *sst) {
         if (c->d_stamps) (void)hipFree(c->d_stamps);
         if (hipMalloc((void **)&c->d_stamps, 8 * 16 * (size_t)a.n_plants) != hipSuccess)
@@ -1257,7 +1211,7 @@ int mpcq_mimo_step_device(mpcq_ctx *c, const double *X, double *U, const double 
     mpcq::MimoArgs a{};
     a.batch = c->dims.batch;
     a.N = c->mimo_N; a.nx = c->mimo_nx; a.nu = c->mimo_nu; a.ny = c->mimo_ny; a.s_rows = c->mimo_srows;
-    a.diag_k0 = c->mimo_diag_k0 && !std::getenv("MPCQ_MIMO_GENERAL_K0");  // (env: force the general path, tests)
+    a.diag_k0 = c->mimo_diag_k0 && !*test_hook("MPCQ_MIMO_GENERAL_K0");
     a.ops_stride = (size_t)mpcq::MimoLayout::make(a.N, a.nx, a.nu, a.ny).total;
     a.ops = c->d_mimo;
     a.st = to_solver(c->set);
@@ -1269,7 +1223,7 @@ int mpcq_mimo_step_device(mpcq_ctx *c, const double *X, double *U, const double 
     a.warm = c->set.warm_start;
     a.fresh = c->fresh;
     a.x = c->d_x; a.y = c->d_y; a.status = c->d_status; a.iter = c->d_iter; a.rho_out = c->d_rho;
-    const char *stp = std::getenv("MPCQ_MIMO_STAMPS");  // debug hook: per-QP stage stamps
+    const char *stp = debug_hook("MPCQ_MIMO_STAMPS");  // per-QP stage stamps
     if (stp && *stp) {
         if (!c->d_stamps && hipMalloc((void **)&c->d_stamps, 8 * 8 * (size_t)a.batch) != hipSuccess)
             return fail(MPCQ_ERR_HIP, "hipMalloc failed (stamps)");

@@ -111,21 +111,6 @@ struct SetupArgs {
                        // 4 the Jacobi eigen-solve hit its sweep cap (inaccurate basis)
 };
 
-// Work-queue schedule of the tile kernel (mpcq_tile.h "Work queue"): the batch is split into
-// kShards contiguous shards, served by the workgroups b with b % nshards == shard (their own
-// counters: the chip's ~3,000 waves would saturate one device-scope word).  Per shard and stage k:
-// tak (claimed; for stage 0 the fresh QPs taken) and res (queued, k >= 1), each on its own 128-B
-// line; then one error word (a wave that polled a queue entry too long).
-constexpr int kMaxStages = 8;
-struct TileSched {
-    static constexpr int kShards = 8;
-    static constexpr int kStride = 32;  // unsigned words per counter line
-    __host__ __device__ static constexpr int tak(int k, int sh) { return ((sh * kMaxStages + k) * 2 + 0) * kStride; }
-    __host__ __device__ static constexpr int res(int k, int sh) { return ((sh * kMaxStages + k) * 2 + 1) * kStride; }
-    __host__ __device__ static constexpr int err() { return kShards * kMaxStages * 2 * kStride; }
-    static constexpr int kWords = (kShards * kMaxStages * 2 + 1) * kStride;
-};
-
 // Phase lists of the tile path: the QPs a phase hands on are appended to one of kShards segments
 // (the appending workgroup's blockIdx % kShards), each with its own counter on its own 128-B line, so
 // the ~3,000 waves reaching a phase boundary together do not serialise on one device-scope counter
@@ -186,16 +171,7 @@ struct AdmmArgs {
     int qp0;                    // QP index of identity-list slot 0 (sub-batch parts of a tile solve)
     int stop_iter;              // phase boundary (multiple of check_termination, or max_iter)
     int resume;                 // 1: phase >= 2 (state, rho and iteration count come from the buffers)
-    long long *stamps;          // debug (MPCQ_TILE_STAMPS): [wave][8] s_memtime / s_memrealtime stamps, or null
-    // tile kernel, work-queue schedule (one launch per solve; mpcq_tile.h "Work queue"): stage k runs
-    // iterations (stops[k-1], stops[k]] of its QPs; QPs still running at stops[k] are handed to stage
-    // k + 1 through qlist.  sched / qlist are zeroed before every launch.
-    int persistent;
-    int nstages;
-    int stops[kMaxStages];
-    unsigned *sched;            // TileSched::kWords counters
-    int *qlist;                 // [stage][batch]: QP index + 1 of the stage's queue (0 = not yet written);
-                                // shard sh's entries start at its first QP index
+    long long *stamps;          // debug build (MPCQ_DEBUG_HOOKS): [wave][8] s_memtime stamps, or null
 };
 
 // MFMA operand images of one shared plant for the tile kernel (mpcq_tile.h).  A vector of length

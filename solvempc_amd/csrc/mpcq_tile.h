@@ -134,20 +134,6 @@ __device__ __forceinline__ int opaque(int v)
     return v;
 }
 
-// Write-through (sc1) store of data another workgroup reads within the launch (work-queue hand-off).
-template <typename V> __device__ __forceinline__ void st_sc1(V *p, V v)
-{
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// A hand-off store: write-through (st_sc1) when a workgroup of the same launch reads it (work queue),
-// a plain write-back store when only a later launch does (phase chain: the kernel boundary publishes
-// it, and the XCD's L2 merges the 16-32 B pieces of a QP row before they reach HBM).
-template <typename V> __device__ __forceinline__ void st_handoff(V *p, V v, bool through)
-{
-    if (through) st_sc1(p, v);
-    else *p = v;
-}
-
 template <typename P> __device__ __forceinline__ P fresh_ptr(P p)
 {
     int zero;
@@ -350,13 +336,17 @@ __device__ __forceinline__ void reg_mv(const T (&m1)[NTO][KS], const T (&x1)[G][
 // z~ for the top half only (z~_{n+j} = -z~_j) and B' w as B~' (w_top - w_bot), and keeps its three
 // operators S, B~', B~ (3 NT KN registers) in VGPRs: no LDS traffic between check iterations.
 // Element 4 s + g of a half-m vector pairs register s with register s + KN (same lane).
-// Debug hook (MPCQ_TILE_STAMPS): per-wave shader-clock stamps at the stage boundaries of a launch:
+// Debug build hook (MPCQ_DEBUG_HOOKS + MPCQ_TILE_STAMPS): per-wave shader-clock stamps at the stage boundaries of a launch:
 // 0 entry, 1 images in LDS, 2 loop entry, 3 phase-boundary save, 4 exit, 5 iteration at exit,
 // 6 / 7 s_memrealtime (100 MHz) at entry / exit.
+#ifdef MPCQ_DEBUG_HOOKS
 #define MPCQ_TSTAMP(k, v)                                                                                  \
     do {                                                                                                   \
         if (a.stamps && (threadIdx.x & 63) == 0) a.stamps[(size_t)(blockIdx.x * WPB + (threadIdx.x >> 6)) * 8 + (k)] = (v); \
     } while (0)
+#else
+#define MPCQ_TSTAMP(k, v) do { } while (0)
+#endif
 // WPB: waves per workgroup (4, or 8 so that an image set serves 8 waves and 4 waves/SIMD fit the LDS).
 template <typename T, int KN, int KM, bool ALL_INEQ, bool LFREE, int G, int OCC, bool PAIRED = false, int WPB = 4>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void admm_tile_kernel(AdmmArgs<T> a)
@@ -467,7 +457,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
 #define MPCQ_PRO_MARK(k) do { } while (0)
 #endif
 
-    const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+    const int lane = threadIdx.x & 63, c = lane & 15;
     constexpr int KNR = PAIRED ? KN : 1, NTR = PAIRED ? NT : 1;
     // f32 paired loop with n = 16 (NT - 1) + 4 (N = 20): the last tile's 4 rows on the 4x4x1 MFMA
     constexpr bool REM4 = PAIRED && std::is_same<T, float>::value && KN % 4 == 1 && NT > 1 && MPCQ_REM4;
@@ -478,25 +468,15 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     const SolverSettings &st = a.st;
     const bool scaled_term = st.scaled_termination != 0;
     const double c64 = (double)op.cs[0];
-    const bool persist = a.persistent != 0;
-    // work queue: this workgroup's shard of the batch, QPs [sh_lo, sh_hi)
-    const unsigned B = (unsigned)a.batch;
-    const unsigned nsh = gridDim.x < (unsigned)TileSched::kShards ? gridDim.x : (unsigned)TileSched::kShards;
-    const unsigned shard = blockIdx.x % nsh;
-    unsigned sh_lo = 0, sh_hi = 0;  // (the divisions only where they are used)
-    if (persist) {
-        sh_lo = (unsigned)((unsigned long long)B * shard / nsh);
-        sh_hi = (unsigned)((unsigned long long)B * (shard + 1) / nsh);
-    }
 
-    // One group of 16 G QPs (column c of group gi: QP b_[gi], live if valid[gi]) from the start of
-    // `stage` to its stop iteration (work queue), or of this launch's phase (phase schedule).
-    auto run_group = [&](const int (&b_)[G], const bool (&valid)[G], const int stage) {
-    // lane indices re-derived opaquely per group, so that no lane-dependent address of the body is
-    // hoisted out of the work-queue loop and held live (in VGPRs) across the hot loop
+    // One group of 16 G QPs (column c of group gi: QP b_[gi], live if valid[gi]) through this
+    // launch's phase.
+    auto run_group = [&](const int (&b_)[G], const bool (&valid)[G]) {
+    // lane indices re-derived opaquely, so that no lane-dependent address of the body is hoisted
+    // and held live (in VGPRs) across the hot loop
     const int lane = opaque((int)threadIdx.x & 63), c = lane & 15, g = lane >> 4;
-    const bool resume = persist ? stage > 0 : a.resume != 0;
-    const bool mpc_fe = persist ? (stage == 0 && a.mpc) : a.mpc != 0;  // front end: the QP's first stage
+    const bool resume = a.resume != 0;
+    const bool mpc_fe = a.mpc != 0;  // front end: the QP's first phase
 
     MPCQ_PRO_MARK(10);
     T uh[G][MS], lh[G][LFREE ? 1 : MS];
@@ -532,7 +512,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                     if (t < nx) s0 += fe[FE_FX + 8 * v + t] * Xv[t];
                 const double s1 = fe[FE_FU + v] * Uv;
                 qk[s] = s0 + s1 + fe[FE_FR + v];
-                if (valid[gi] && v < n) st_handoff(a.q_out + (size_t)b * n + v, qk[s], persist);  // read by later stages
+                if (valid[gi] && v < n) a.q_out[(size_t)b * n + v] = qk[s];  // read by later phases
             }
             MPCQ_PRO_MARK(11);
 #pragma unroll
@@ -543,7 +523,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 for (int t = 0; t < 8; t++)
                     if (t < nx) sx += fe[FE_SB + 8 * v + t] * Xv[t];
                 up[s] = fe[FE_W0 + v] + sx + fe[FE_KU + v] * Uv;
-                if (valid[gi] && v < m) st_handoff(a.u_out + (size_t)b * m + v, up[s], persist);
+                if (valid[gi] && v < m) a.u_out[(size_t)b * m + v] = up[s];
             }
             MPCQ_PRO_MARK(12);
         } else {
@@ -724,10 +704,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     }
 
     MPCQ_PRO_MARK(5);
-    long long info_cycles = 0;
+    [[maybe_unused]] long long info_cycles = 0;  // (debug build: cycles in info iterations)
     const int ct = st.check_termination;
     const int ai = (st.adaptive_rho && a.adaptive_interval) ? a.adaptive_interval : 0;
-    const int stop = persist ? a.stops[stage] : a.stop_iter;
+    const int stop = a.stop_iter;
     int next_check = ct ? (it / ct + 1) * ct : -1;  // uniform; no integer division in the loop
     int next_adapt = ai ? (it / ai + 1) * ai : -1;
     T dx[G][NS], dy[G][MS];
@@ -961,7 +941,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             }
         }
     };
-    if (!persist) MPCQ_TSTAMP(2, (long long)__builtin_amdgcn_s_memtime());
+    MPCQ_TSTAMP(2, (long long)__builtin_amdgcn_s_memtime());
     while (!all_done()) {
         if constexpr (PAIRED) {
             // plain iterations up to the next info iteration, with the operators held in VGPRs
@@ -1393,11 +1373,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
         if (a.stamps) info_cycles += (long long)__builtin_amdgcn_s_memtime() - t_info;
 #endif
         if (it == stop && !all_done()) {
-            if (!persist) MPCQ_TSTAMP(3, (long long)__builtin_amdgcn_s_memtime());
-            // stage / phase boundary: save the running QPs and queue them for the next stage / launch.
-            // Work queue: the state is another workgroup's input within this launch, so it is stored
-            // write-through (sc1) and drained before the queue entries (the flags) are written
-            // (cdna_hip_programming.md G16 recipe R1; the consumer polls the entries, then acquires).
+            MPCQ_TSTAMP(3, (long long)__builtin_amdgcn_s_memtime());
+            // phase boundary: save the running QPs and list them for the next launch (the kernel
+            // boundary publishes the stores; the XCD's L2 merges a QP row's 16-32 B pieces)
 #pragma unroll
             for (int gi = 0; gi < G; gi++) {
                 const bool run = !done[gi];
@@ -1405,20 +1383,19 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 if (run) {
 #pragma unroll
                     for (int s = 0; s < NS; s++)
-                        if (s < KN) st_handoff(a.xs + (size_t)b * ncs + 4 * s + g, xs[gi][s], persist);
+                        if (s < KN) a.xs[(size_t)b * ncs + 4 * s + g] = xs[gi][s];
 #pragma unroll
                     for (int s = 0; s < MS; s++)
                         if (s < KM) {
-                            st_handoff(a.zs + (size_t)b * mcs + 4 * s + g, z[gi][s], persist);
-                            st_handoff(a.ys + (size_t)b * mcs + 4 * s + g, y[gi][s], persist);
+                            a.zs[(size_t)b * mcs + 4 * s + g] = z[gi][s];
+                            a.ys[(size_t)b * mcs + 4 * s + g] = y[gi][s];
                         }
                     if (g == 0) {
-                        st_handoff(a.rhos + b, rho[gi], persist);
-                        st_handoff(a.it_state + b, it, persist);
+                        a.rhos[b] = rho[gi];
+                        a.it_state[b] = it;
                     }
                 }
             }
-            if (persist) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (work queue: before the flags)
             unsigned long long mask[G];
             unsigned total = 0;
 #pragma unroll
@@ -1427,204 +1404,64 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 total += (unsigned)__popcll(mask[gi]);
             }
             int base = 0;
-            if (lane == 0)
-                base = persist ? (int)__hip_atomic_fetch_add(a.sched + TileSched::res(stage + 1, shard), total,
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                               : atomicAdd(a.count_out + (blockIdx.x % ListSeg::kShards) * ListSeg::kStride, (int)total);
+            if (lane == 0) base = atomicAdd(a.count_out + (blockIdx.x % ListSeg::kShards) * ListSeg::kStride, (int)total);
             base = __shfl(base, 0);
-            int *const qout = persist ? a.qlist + (size_t)(stage + 1) * a.batch + sh_lo
-                                      : a.list_out + (blockIdx.x % ListSeg::kShards) * a.list_seg;
+            int *const qout = a.list_out + (blockIdx.x % ListSeg::kShards) * a.list_seg;
 #pragma unroll
             for (int gi = 0; gi < G; gi++) {
                 const unsigned long long below = (1ull << c) - 1ull;  // the column's g = 0 lane is lane c
                 int pos = base + __popcll(mask[gi] & below);
 #pragma unroll
                 for (int gj = 0; gj < gi; gj++) pos += __popcll(mask[gj]);
-                if (!done[gi] && g == 0) {
-                    const int b = opaque(b_[gi]);
-                    if (persist) st_sc1(qout + pos, b + 1);  // the flag a consumer polls
-                    else qout[pos] = b;
-                }
+                if (!done[gi] && g == 0) qout[pos] = opaque(b_[gi]);
             }
             break;
         }
     }
 #ifndef MPCQ_PRO_PART
-    if (!persist) MPCQ_TSTAMP(5, info_cycles);  // cycles in info iterations (checks, adapt, stop)
+    MPCQ_TSTAMP(5, info_cycles);  // cycles in info iterations (checks, adapt, stop)
 #endif
     };  // run_group
 
-    // ---- Work queue (one launch per solve).  After each group a wave claims 16 G QPs of its shard:
-    // fresh QPs of stage 0 first (they carry the most remaining work), else a full group of the
-    // lowest continuation stage that has one, else the remainder of the lowest non-empty stage; it
-    // leaves when its shard has nothing queued.  Nothing is orphaned: a wave that hands QPs on claims
-    // again afterwards, so the last wave of a shard drains its queues.  Claims are atomic (fetch-add
-    // on the fresh counter, compare-and-swap on a stage's tak); no wave ever waits for work.  The
-    // phase schedule runs the loop once, on the wave's slots of the launch's list.  (One call site:
-    // run_group is inlined once.)
-    unsigned *const S = a.sched;
-    const unsigned NSTG = (unsigned)a.nstages;
-    constexpr unsigned WANT = 16 * G;
-    constexpr unsigned kMaxPolls = 1u << 21;
-    auto ld = [](const unsigned *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-    bool first = true, fresh_left = true;
-    long long st_groups = 0, st_qps = 0, st_busy = 0;  // debug stamps (work queue): groups, QPs, cycles in groups
-    for (;;) {
-        int k = -2;
-        unsigned base = 0, cnt = 0;
-        if (!persist) {
-            // phase schedule: this wave's 16 G QPs are slots wave_slot.. of the launch's list
-            const int wave_slot = (blk * WPB + (threadIdx.x >> 6)) * 16 * G;
-            if (!first || wave_slot >= count) break;
-            k = 0;
-            base = (unsigned)wave_slot;
-            cnt = (unsigned)(count - wave_slot);
-        } else if (lane == 0) {
-            const unsigned nfresh = sh_hi - sh_lo;
-            if (fresh_left) {
-                const unsigned t = __hip_atomic_fetch_add(S + TileSched::tak(0, shard), WANT, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT);
-                if (t < nfresh) { k = 0; base = sh_lo + t; cnt = nfresh - t < WANT ? nfresh - t : WANT; }
-                else fresh_left = false;
-            }
-            for (int tries = 0; k == -2 && tries < 64; tries++) {
-                unsigned res[kMaxStages], tak[kMaxStages];
-#pragma unroll
-                for (int s = 1; s < kMaxStages; s++)
-                    if (s < (int)NSTG) {
-                        res[s] = ld(S + TileSched::res(s, shard));
-                        tak[s] = ld(S + TileSched::tak(s, shard));
-                    }
-                int pick = -1;
-                unsigned p_res = 0, p_tak = 0;  // (no runtime-indexed arrays: they would live in scratch)
-#pragma unroll
-                for (int s = kMaxStages - 1; s >= 1; s--)  // lowest full stage, else lowest non-empty
-                    if (s < (int)NSTG && res[s] > tak[s] &&
-                        (pick < 0 || res[s] - tak[s] >= WANT || p_res - p_tak < WANT)) {
-                        pick = s;
-                        p_res = res[s];
-                        p_tak = tak[s];
-                    }
-                if (pick < 0) { k = -1; break; }  // the shard has nothing queued: leave
-                const unsigned avail = p_res - p_tak, want = avail < WANT ? avail : WANT;
-                unsigned expect = p_tak;
-                if (__hip_atomic_compare_exchange_strong(S + TileSched::tak(pick, shard), &expect, p_tak + want,
-                                                         __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                    k = pick; base = p_tak; cnt = want;
-                }
-            }
-            if (k == -2) k = -1;  // 64 lost races in a row: leave (the winners drain the queue)
-        }
-        first = false;
-        k = __builtin_amdgcn_readfirstlane(k);
-        base = __builtin_amdgcn_readfirstlane(base);
-        cnt = __builtin_amdgcn_readfirstlane(cnt);
-        fresh_left = __builtin_amdgcn_readfirstlane((int)fresh_left) != 0;
-        if (k < 0) break;
+    // this wave's 16 G QPs: slots wave_slot.. of the launch's list (or of the batch in phase 0)
+    const int wave_slot = (blk * WPB + (threadIdx.x >> 6)) * 16 * G;
+    if (wave_slot < count) {
         bool valid[G];
         int b_[G];
-        if (k == 0) {
 #pragma unroll
-            for (int gi = 0; gi < G; gi++) {
-                const unsigned slot = 16 * gi + c;
-                valid[gi] = slot < cnt;
-                const int i = (int)(base + slot) + (seglist ? seg * a.list_seg : 0);  // list entry
-                b_[gi] = valid[gi] ? (seglist ? a.list_in[i] : a.qp0 + i) : 0;
-            }
-        } else {
-            // the entries were reserved before this claim; poll until their producers wrote them
-            const int *q = a.qlist + (size_t)k * B + sh_lo + base;
-            bool ok = false;
-            for (unsigned sp = 0; sp < kMaxPolls; sp++) {
-                bool all = true;
-#pragma unroll
-                for (int gi = 0; gi < G; gi++) {
-                    const unsigned slot = 16 * gi + c;
-                    valid[gi] = slot < cnt;
-                    b_[gi] = valid[gi] ? __hip_atomic_load(q + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1 : 0;
-                    all = all && (!valid[gi] || b_[gi] >= 0);
-                }
-                if (wave_all(all)) { ok = true; break; }
-                __builtin_amdgcn_s_sleep(2);
-            }
-            if (!ok) {
-                if (lane == 0) __hip_atomic_store(S + TileSched::err(), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-            // acquire: the state behind the entries (stored sc1 and drained by their producers)
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (int gi = 0; gi < G; gi++) {
+            const int slot = wave_slot + 16 * gi + c;
+            valid[gi] = slot < count;
+            const int i = slot + (seglist ? seg * a.list_seg : 0);  // list entry
+            b_[gi] = valid[gi] ? (seglist ? a.list_in[i] : a.qp0 + i) : 0;
         }
-        const long long t_run = a.stamps ? (long long)__builtin_amdgcn_s_memtime() : 0;
-        run_group(b_, valid, k);
-        if (a.stamps) {
-            st_groups++;
-            st_qps += cnt;
-            st_busy += (long long)__builtin_amdgcn_s_memtime() - t_run;
-        }
-    }
-    if (persist) {
-        MPCQ_TSTAMP(2, st_groups);
-        MPCQ_TSTAMP(3, st_qps);
-        MPCQ_TSTAMP(5, st_busy);
+        run_group(b_, valid);
     }
     MPCQ_TSTAMP(4, (long long)__builtin_amdgcn_s_memtime());
     MPCQ_TSTAMP(7, (long long)__builtin_amdgcn_s_memrealtime());
 }
 
-// Launch one tile-kernel variant: one workgroup per 64 G QPs (phase schedule), or for the work
-// queue at most as many workgroups as are resident at once (the kernel's occupancy x CUs, cached per
-// variant), each looping over claimed groups.
+// Launch one tile-kernel variant: one workgroup per 64 G QPs of the phase's grid.
 template <typename T, int KN, int KM, bool AI, bool LF, int G, int OCC, bool PAIRED = false, int WPB = 4>
 int tile_launch_variant(const AdmmArgs<T> &a, hipStream_t s)
 {
-    auto kern = admm_tile_kernel<T, KN, KM, AI, LF, G, OCC, PAIRED, WPB>;
     constexpr int QPW = 16 * G * WPB;
-    int blocks = (a.batch + QPW - 1) / QPW;
-    if (a.persistent) {
-        static int resident = 0;
-        if (!resident) {
-            int per_cu = 0, dev = 0, cus = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * WPB, 0) != hipSuccess ||
-                hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu < 1)
-                return -2;
-            resident = per_cu * cus;
-        }
-        blocks = blocks < resident ? blocks : resident;
-    }
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * WPB), 0, s, a);
+    const int blocks = (a.batch + QPW - 1) / QPW;
+    hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, AI, LF, G, OCC, PAIRED, WPB>), dim3(blocks), dim3(64 * WPB), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-// occ: 0 = default for the shape/type, else a requested variant (benchmark A/B hook):
-// f32 paired loop: default 1 group/wave at 3 waves/SIMD;  occ 2 -> 2 groups/wave at 2 waves/SIMD;
-// occ 4 -> 4 waves/SIMD (LDS-limited to 3 workgroups per CU: only with a smaller image set; measured
-// with W, W' out of LDS at 128 VGPRs: spills, 0.50 vs 0.44 ms per cfg2 solve).
+// One variant per shape and type (measured A/B): f32 runs one 16-QP group per
+// wave at 3 waves/SIMD, f64 at 2 (2 groups per wave, 4 waves/SIMD and 8-wave workgroups were slower).
 template <typename T, int KN, int KM>
-int tile_launch(const AdmmArgs<T> &a, int occ, hipStream_t s)
+int tile_launch(const AdmmArgs<T> &a, hipStream_t s)
 {
+    constexpr int OCC = sizeof(T) == 8 ? 2 : 3;
     if constexpr (KM == 2 * KN) {
-        if (a.paired && a.all_ineq && a.lower_free) {  // the condensed-MPC shape: paired, VGPR-resident loop
-            if constexpr (sizeof(T) == 8) {
-                return tile_launch_variant<T, KN, KM, true, true, 1, 2, true>(a, s);
-            } else {
-                if (occ == 2) return tile_launch_variant<T, KN, KM, true, true, 2, 2, true>(a, s);
-                if (occ == 4) return tile_launch_variant<T, KN, KM, true, true, 1, 4, true>(a, s);
-                if (occ == 8) return tile_launch_variant<T, KN, KM, true, true, 1, 4, true, 8>(a, s);
-                return tile_launch_variant<T, KN, KM, true, true, 1, 3, true>(a, s);
-            }
-        }
+        if (a.paired && a.all_ineq && a.lower_free)  // the condensed-MPC shape: paired, VGPR-resident loop
+            return tile_launch_variant<T, KN, KM, true, true, 1, OCC, true>(a, s);
     }
-    if (a.all_ineq && a.lower_free) {
-        if constexpr (sizeof(T) == 8) {
-            if (occ == 1) return tile_launch_variant<T, KN, KM, true, true, 2, 1>(a, s);
-            return tile_launch_variant<T, KN, KM, true, true, 1, 2>(a, s);
-        } else {
-            if (occ == 2) return tile_launch_variant<T, KN, KM, true, true, 2, 2>(a, s);
-            return tile_launch_variant<T, KN, KM, true, true, 1, 3>(a, s);
-        }
-    }
+    if (a.all_ineq && a.lower_free) return tile_launch_variant<T, KN, KM, true, true, 1, OCC>(a, s);
     return tile_launch_variant<T, KN, KM, false, false, 1, 2>(a, s);
 }
 
@@ -1635,9 +1472,7 @@ int tile_launch(const AdmmArgs<T> &a, int occ, hipStream_t s)
 template <typename T>
 int tile_launch_any(const AdmmArgs<T> &a, int KN, int KM, hipStream_t s)
 {
-    const char *e = getenv("MPCQ_TILE_OCC");
-    const int occ = e ? atoi(e) : 0;
-#define MPCQ_TRY(KN_, KM_) if (KN == KN_ && KM == KM_) return tile_launch<T, KN_, KM_>(a, occ, s);
+#define MPCQ_TRY(KN_, KM_) if (KN == KN_ && KM == KM_) return tile_launch<T, KN_, KM_>(a, s);
     MPCQ_TILE_SHAPES(MPCQ_TRY)
 #undef MPCQ_TRY
     return -1;

@@ -8,6 +8,11 @@ Bar, asserted on EVERY QP of every case:
   relative because fp32 carries 24 bits: moves reach |x0| ~ 75 here, where one fp32 ulp is 7.6e-6,
   and the ADMM iterate accumulates ~2e-6 relative over its ~100 iterations (measured max 2.7e-5
   absolute at |x| ~ 60); the absolute 1e-5 is the fp64 path's bar.
+  Exception, counted and bounded: a QP whose schedule decision the oracle itself takes within
+  TIE_MARGIN of its threshold (|ln(residual / tolerance)| < 2e-3, oracle Info.margin; ~0.1% of QPs)
+  can take the other branch in fp32, whose residuals carry ~1e-3 relative rounding.  Such a QP must
+  still end SOLVED with the OSQP termination criteria met by the device's own solution (a valid
+  OSQP answer one check earlier or later), and the test reports how many did.
 Full-size (65,536 QP) runs are checked through size-independent properties (KKT residuals at the
 solver's own tolerance) and shard invariance against the oracle on a prefix.
 """
@@ -23,6 +28,34 @@ from solvempc_amd import workload
 pytestmark = pytest.mark.gpu
 LMIN = -np.finfo(np.float64).max
 F32_TOL = 1e-5
+
+
+TIE_MARGIN = 2e-3
+
+
+def _f32_parity(s, x, st, it, x_ref, st_ref, it_ref, margin, q, u, ops, what=""):
+    """The fp32 bar on every QP (module docstring): returns the number of schedule ties taken the
+    other way."""
+    assert np.array_equal(st, st_ref), what
+    tie = margin < TIE_MARGIN
+    off = it != it_ref
+    assert not np.any(off & ~tie), (what, np.flatnonzero(off & ~tie)[:8], margin[off & ~tie][:8])
+    _f32_close(x[~off], x_ref[~off], what)
+    if off.any():  # the other branch of a tie: a valid OSQP answer of its own
+        _osqp_terminated(x[off], s.dual()[off], q[off], u[off], ops)
+    return int(off.sum())
+
+
+def _osqp_terminated(x, y, q, u, ops, slack=1.5):
+    """Unscaled primal / dual residuals within OSQP's eps_abs = eps_rel = 1e-3 tolerances."""
+    Ax = x @ ops["A"].T
+    prim = np.maximum(Ax - u, 0).max(axis=1)
+    tol_p = 1e-3 + 1e-3 * np.maximum(np.abs(Ax).max(axis=1), np.abs(u).max(axis=1))
+    assert np.all(prim <= slack * tol_p)
+    Px, Aty = x @ ops["P"], y @ ops["A"]
+    dual = np.abs(Px + q + Aty).max(axis=1)
+    tol_d = 1e-3 + 1e-3 * np.maximum(np.abs(q).max(axis=1), np.maximum(np.abs(Aty).max(axis=1), np.abs(Px).max(axis=1)))
+    assert np.all(dual <= slack * tol_d)
 
 
 def _f32_close(x, x_ref, what=""):
@@ -66,10 +99,10 @@ def _gpu_solve(ops, q, u, N, dtype="f64", settings=None):
     return s
 
 
-def _oracle_solve(ops, q, u, N, settings=None):
+def _oracle_solve(ops, q, u, N, settings=None, margins=False):
     l = np.full(2 * N, LMIN)
     return oracle.batch_solve(ops["P"], ops["A"], np.zeros(N), l, oracle.upper_bound(ops, np.zeros(4), 0.0),
-                              q, u, settings=settings)
+                              q, u, settings=settings, margins=margins)
 
 
 @pytest.mark.parametrize("N,u_range", [(20, 1.0), (15, 0.0)])
@@ -88,13 +121,13 @@ def test_fp64_trajectory_parity(plant, N, u_range, kernel):
 @pytest.mark.parametrize("N,seed", [(20, 1), (15, 3)])
 def test_fp32_parity(plant, kernel, N, seed):
     ops, X, U, q, u = _problem(plant, N, 4096, seed=seed)
-    x_ref, st_ref, it_ref, _ = _oracle_solve(ops, q, u, N)
+    x_ref, st_ref, it_ref, _, margin = _oracle_solve(ops, q, u, N, margins=True)
     s = _gpu_solve(ops, q, u, N, dtype="f32")
     x = s.solution()
     st, it, _ = s.info()
-    assert np.array_equal(st, st_ref) and np.all(st == sm.SOLVED)
-    assert np.array_equal(it, it_ref), f"{np.mean(it != it_ref):.3%} of QPs off the oracle's iteration schedule"
-    _f32_close(x, x_ref)
+    assert np.all(st == sm.SOLVED)
+    ties = _f32_parity(s, x, st, it, x_ref, st_ref, it_ref, margin, q, u, ops)
+    print(f"fp32 N={N} seed={seed}: {ties} of 4096 QPs took a tie's other branch")
 
 
 def test_f64_absolute_bound(plant):
@@ -240,12 +273,14 @@ def test_full_batch_kkt_properties(plant, dtype):
     tol_d = 1e-3 + 1e-3 * np.maximum(np.abs(q).max(axis=1), np.maximum(np.abs(Aty).max(axis=1), np.abs(Px).max(axis=1)))
     assert np.all(dual <= 1.5 * tol_d)
     # shard invariance: the first 1,024 QPs of the full batch are the oracle's
-    x_ref, st_ref, it_ref, _ = _oracle_solve(ops, q[:1024], u[:1024], N)
-    assert np.array_equal(it[:1024], it_ref)
+    x_ref, st_ref, it_ref, _, margin = _oracle_solve(ops, q[:1024], u[:1024], N, margins=True)
     if dtype == "f64":
+        assert np.array_equal(it[:1024], it_ref)
         assert np.abs(x[:1024] - x_ref).max() < 1e-9
     else:
-        _f32_close(x[:1024], x_ref)
+        off = it[:1024] != it_ref
+        assert not np.any(off & (margin >= TIE_MARGIN))
+        _f32_close(x[:1024][~off], x_ref[~off])
 
 
 def test_max_iter_and_warm_start(plant, kernel):
@@ -331,6 +366,7 @@ def test_tile_and_wave_paths_agree(plant):
     |dx| <= 1e-9, fp32 within F32_TOL * max(1, ||x||_inf)."""
     N = 20
     ops, X, U, q, u = _problem(plant, N, 2048, seed=21)
+    margin = _oracle_solve(ops, q, u, N, margins=True)[4]
     for dtype in ("f64", "f32"):
         res = {}
         for k in ("tile", "wave"):
@@ -346,8 +382,9 @@ def test_tile_and_wave_paths_agree(plant):
             assert np.array_equal(itt, itw)
             assert np.abs(xt - xw).max() <= 1e-9
         else:
-            assert np.array_equal(itt, itw)
-            _f32_close(xt, xw, "tile vs wave")
+            off = itt != itw
+            assert not np.any(off & (margin >= TIE_MARGIN))
+            _f32_close(xt[~off], xw[~off], "tile vs wave")
 
 
 def test_plant_simulation_matches_host(plant):
@@ -423,6 +460,7 @@ def test_receding_horizon_stream_f32(plant, kernel):
     st = torch.cuda.Stream()
     refs = [oracle.Solver(ops["P"], np.zeros(N), ops["A"], l, u0) for _ in range(B)]
     Xk, Uk = X.copy(), U.copy()
+    tied = set()  # plants whose warm state left the oracle's at a schedule tie: no longer compared
     for k in range(steps):
         with torch.cuda.stream(st):
             s.mpc_run_device(Xd.data_ptr(), Ud.data_ptr(), 0.0, 1, 9, 0, k, 1e-2, st.cuda_stream)
@@ -430,14 +468,20 @@ def test_receding_horizon_stream_f32(plant, kernel):
         stat, it, _ = s.info()
         Ug = Ud.cpu().numpy()
         for b, r in enumerate(refs):
+            if b in tied:
+                continue
             assert r.update_gradient(oracle.gradient(ops, Xk[b], Uk[b]))
             assert r.update_upper_bound(oracle.upper_bound(ops, Xk[b], Uk[b]))
             assert r.solve() == oracle.SOLVED and stat[b] == sm.SOLVED
-            assert it[b] == r.info().iter, (k, b, it[b], r.info().iter)
+            if it[b] != r.info().iter:  # a schedule tie (module docstring)
+                assert r.info().margin < TIE_MARGIN, (k, b, it[b], r.info().iter, r.info().margin)
+                tied.add(b)
+                continue
             x = r.x()
             assert abs(Ug[b] - (Uk[b] + x[0])) < F32_TOL * max(1.0, np.abs(x).max()), (k, b)
         Uk = Ug.copy()
         Xk = Xd.cpu().numpy().copy()
+    assert len(tied) <= 2, tied
 
 
 def test_stream_workload_stays_solved_and_bounded(plant):
@@ -563,7 +607,11 @@ def test_per_plant_device_pipeline(plant, dtype):
         assert r.update_gradient(oracle.gradient(ops, X[b], U[b]))
         assert r.update_upper_bound(oracle.upper_bound(ops, X[b], U[b]))
         st_o = r.solve()
-        assert st[b] == st_o and it[b] == r.info().iter, b
+        assert st[b] == st_o, b
+        if dtype == "f32" and it[b] != r.info().iter:  # a schedule tie (module docstring)
+            assert r.info().margin < TIE_MARGIN, (b, it[b], r.info().iter, r.info().margin)
+            continue
+        assert it[b] == r.info().iter, b
         u_ref = U[b] + (r.x()[0] if st_o == sm.SOLVED else 0.0)
         tol = 1e-9 if dtype == "f64" else F32_TOL * max(1.0, np.abs(r.x()).max())
         assert abs(Ug[b] - u_ref) < tol, (b, Ug[b] - u_ref)
@@ -619,49 +667,27 @@ def test_stream_graph_recaptured_after_replant(plant):
 
 def test_paired_tile_path_selected(plant):
     """The reference's constraint matrix Gbar = [K0 L; -K0 L] (ModelPredictiveControlAPI.cpp:332-347)
-    puts a shared-plant batch on the tile kernel's paired loop; a generic A does not."""
-    N = 20
-    ops, X, U, q, u = _problem(plant, N, 64)
+    puts a shared-plant batch on the tile kernel's paired loop; a generic A does not; batches under
+    8,192 QPs run one QP per wave (the path mpcq_get_path reports is the one launch_args runs)."""
+    N, B = 20, 8192
+    ops, X, U, q, u = _problem(plant, N, B)
     s = _gpu_solve(ops, q, u, N, dtype="f32")
     assert s.path() == ("tile", True)
     A = ops["A"].copy()
     A[N + 3, 0] *= 1.0000001  # no longer an exact negation of row 3
-    s2 = sm.BatchSolver(N, 2 * N, 64, dtype="f32")
+    s2 = sm.BatchSolver(N, 2 * N, B, dtype="f32")
     s2.setup(ops["P"], np.zeros(N), A, np.full(2 * N, LMIN), ops["W0"])
     assert s2.path() == ("tile", False)
-
-
-def test_tile_work_queue_schedule(plant, monkeypatch):
-    """The experimental one-launch work-queue schedule of the tile path (MPCQ_TILE_SCHED=queue) against
-    the default phase chain: it finishes the slow tail in the tile kernel instead of the
-    one-QP-per-wave kernel (other summation order there), so: the same status, and in f64 the same
-    iterations and |dx| <= 1e-9."""
-    N, B = 20, 16384
-    ops, X, U, q, u = _problem(plant, N, B, seed=23)
-    for dtype in ("f64", "f32"):
-        res = {}
-        for name, env in (("one", {}), ("queue", {"MPCQ_TILE_SCHED": "queue"})):
-            for k, v in env.items():
-                monkeypatch.setenv(k, v)
-            s = _gpu_solve(ops, q, u, N, dtype=dtype)
-            res[name] = (s.solution(), *s.info())
-            for k in env:
-                monkeypatch.delenv(k)
-        x1, st1, it1, r1 = res["one"]
-        assert np.all(st1 == sm.SOLVED)
-        x3, st3, it3, _ = res["queue"]
-        assert np.array_equal(st1, st3), dtype
-        if dtype == "f64":
-            assert np.array_equal(it1, it3) and np.abs(x1 - x3).max() <= 1e-9
+    s3 = _gpu_solve(ops, q[:64], u[:64], N, dtype="f32")
+    assert s3.path() == ("wave", False)
 
 
 @pytest.mark.gpu
 def test_phase_chain_counters_across_solves(plant, monkeypatch):
     """One context, consecutive cold solves whose phase chains differ in length (default, one launch,
     two launches, default again): the list counters the launches keep clean themselves (no per-solve
-    memset) must hand every QP on, so each solve gives the first one's statuses (f64: iterations and
-    |dx| <= 1e-9; the one-launch schedule finishes the tail in the tile kernel, other summation
-    order) and the two default solves are bit-identical."""
+    memset) must hand every QP on, so each solve gives the first one's statuses, iterations and
+    |dx| <= 1e-9 (f64), and the two default solves are bit-identical."""
     N, B = 20, 16384
     ops, X, U, q, u = _problem(plant, N, B, seed=29)
     s = _gpu_solve(ops, q, u, N, dtype="f64")
