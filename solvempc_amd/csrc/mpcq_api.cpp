@@ -78,6 +78,7 @@ struct mpcq_ctx {
     enum class Mode { None, Generic, Mimo } mode = Mode::None;
     bool all_ineq = true, mpc_ready = false, lower_free = false, fresh = false;
     bool paired = false;  // shared plant of the condensed-MPC shape (tile kernel's paired loop)
+    bool inv_ops = false; // per-plant operators in the direct-inverse reading (setup_inv_kernel): wave kernel only
     // tile (MFMA) path: shared plant with a compiled (KN, KM) shape
     bool tile = false;
     int KN = 0, KM = 0;
@@ -457,10 +458,19 @@ int setup_on_device(mpcq_ctx *c, hipStream_t s)
     a.ctype = c->d_ctype;
     a.status = c->d_setup_status;
     a.flags = c->d_flags;
-    // one wavefront per plant, LDS-resident (mpcq_setup_wave.hip) where the plant fits; the
-    // global-scratch workgroup kernel otherwise (MPCQ_SETUP=ref forces it: A/B test hook)
-    const bool ref_setup = !std::strcmp(test_hook("MPCQ_SETUP"), "ref") || !mpcq_internal_setup_wave_lds((int)n, (int)m);
-    if (ref_setup) {
+    // One wavefront per plant, LDS-resident (mpcq_setup_wave.hip), where the plant fits: per-plant
+    // batches take the direct inverse of M(rho) (no eigen-solve: their QPs are solved once or a few
+    // times each), a shared plant the eigen-basis (every QP of the batch reuses it, whatever rho it
+    // reaches; the tile kernel's images).  The global-scratch workgroup kernel (eigen-basis) serves
+    // larger plants.  Test hook MPCQ_SETUP: "ref" forces the workgroup kernel, "eigen" the wave
+    // kernel's eigen-basis for per-plant batches.
+    const char *hook = test_hook("MPCQ_SETUP");
+    const bool fits = mpcq_internal_setup_wave_lds((int)n, (int)m) != 0;
+    const bool ref_setup = !std::strcmp(hook, "ref") || !fits;
+    c->inv_ops = !ref_setup && Pn > 1 && std::strcmp(hook, "eigen") != 0;
+    if (c->inv_ops) {
+        if (mpcq_internal_setup_inv_launch(&a, s) != 0) return fail(MPCQ_ERR_HIP, "setup kernel launch failed");
+    } else if (ref_setup) {
         if (!c->d_scratch && hipMalloc((void **)&c->d_scratch, 8 * Pn * setup_scratch_len((int)n, (int)m)) != hipSuccess)
             return fail(MPCQ_ERR_HIP, "hipMalloc failed (setup scratch)");
         a.scratch = c->d_scratch;
@@ -493,7 +503,7 @@ int setup_on_device(mpcq_ctx *c, hipStream_t s)
     HIPCHK(hipMemcpyAsync(&flags, c->d_flags, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(blk.data(), c->d_ops, 8 * c->ops_stride, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    if (flags & 1) return fail(MPCQ_ERR_SETUP, "setup: P + sigma I not positive definite (non-convex QP)");
+    if (flags & 1) return fail(MPCQ_ERR_SETUP, "setup: P + sigma I (+ rho A'A) not positive definite (non-convex QP)");
     if (flags & 4) return fail(MPCQ_ERR_SETUP, "setup: Jacobi eigen-solve of the KKT family did not converge in 60 sweeps");
     c->all_ineq = !(flags & 2);
     for (size_t i = 0; i < n; i++) c->hD[i] = blk[L.D + i];
@@ -733,6 +743,7 @@ static PathChoice choose_path(const mpcq_ctx *c)
     const char *k = env_kernel();
     const bool fits_wave = c->dims.n <= 32 && c->dims.m <= 64;
     PathChoice p{MPCQ_PATH_LANE, false};
+    if (c->inv_ops) return {MPCQ_PATH_WAVE, false};  // direct-inverse operators: the wave kernel's refactorisation
     if (std::strcmp(k, "lane") == 0 || !fits_wave) return p;
     if (!c->tile) return {MPCQ_PATH_WAVE, false};
     const bool small = c->dims.batch < 8192 && std::strcmp(k, "tile") != 0;

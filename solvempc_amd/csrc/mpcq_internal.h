@@ -1,14 +1,18 @@
 // solvempc_amd/csrc/mpcq_internal.h — device data layout shared by the setup and ADMM kernels.
 //
-// Factorisation used on the device (replaces OSQP's QDLDL LDL' of the KKT matrix): for a plant
+// Factorisations used on the device (replace OSQP's QDLDL LDL' of the KKT matrix): for a plant
 // with scaled data (P^, A^) and constraint-type pattern s (rho_j = rho*s_j, or RHO_MIN for free
 // rows), the reduced KKT matrix is a one-parameter family
 //        M(rho) = P~ + rho G,   P~ = P^ + sigma I + RHO_MIN sum_free a_j a_j',  G = sum s_j a_j a_j'.
-// Setup computes the generalised eigen-basis  W' P~ W = I,  W' G W = diag(lambda), so that
-//        M(rho)^-1 = W diag(1/(1 + rho lambda)) W'
-// for EVERY rho.  An adaptive-rho update (OSQP adapt_rho) therefore only rescales a diagonal:
-// no refactorisation, and all QPs of a plant share W whatever rho each one has reached.
-// The ADMM iterate keeps x in that basis (x^ = W x'); see mpcq_admm.hip.
+// * Eigen-basis (shared plants; per-plant shapes beyond one wave): setup computes W' P~ W = I,
+//   W' G W = diag(lambda), so that M(rho)^-1 = W diag(1/(1 + rho lambda)) W' for EVERY rho: an
+//   adaptive-rho update (OSQP adapt_rho) only rescales a diagonal, and all QPs of a plant share W
+//   whatever rho each one has reached.  The iterate keeps x in that basis (x^ = W x').
+// * Direct inverse (per-plant batches, n <= 32, m <= 64; setup_inv_kernel): M(rho0)^-1 itself, the
+//   iterate in the scaled basis (x' = x^).  The same operator slots then hold W = W^-1 = I,
+//   lambda = 0, sigma W'W = sigma M^-1, G = M^-1, Bt = A^ M^-1 (so one iteration is the same code
+//   for both), and rho0 = the rho they were built for; a QP whose rho moves away from rho0 rebuilds
+//   M^-1 in its kernel (OSQP's refactorisation, mpcq_wave.h).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -43,11 +47,13 @@ struct PlantOps {
     const T *rscale; // MC          rho_j = rho * rscale_j  (0 => free row => RHO_MIN)
     const int *ctype;// MC          OSQP constr_type: -1 free, 0 inequality, 1 equality
 };
+// (G: NC x NC, g = -G' q^; Bt: MC x NC, the x-side product's operator rows; rho0: 1.  Eigen-basis:
+// G = W, Bt = A^ W, rho0 = -1.  Direct inverse: G = M^-1, Bt = A^ M^-1, rho0 = the built-for rho.)
 
 // Shapes of one plant's operator block, in elements, for capacities (nc, mc).
 struct OpsLayout {
     int nc, mc;
-    size_t lam, W, sWtW, WtA, PW, Winv, Ah, D, E, Dinv, Einv, cs, rscale, total;
+    size_t lam, W, sWtW, WtA, PW, Winv, Ah, D, E, Dinv, Einv, cs, rscale, G, Bt, rho0, total;
     __host__ __device__ static constexpr OpsLayout make(int nc, int mc)
     {
         OpsLayout L{};
@@ -67,6 +73,9 @@ struct OpsLayout {
         L.Einv = o; o += mc;
         L.cs = o; o += 2;
         L.rscale = o; o += mc;
+        L.G = o; o += (size_t)nc * nc;
+        L.Bt = o; o += (size_t)mc * nc;
+        L.rho0 = o; o += 2;
         L.total = o;
         return L;
     }
@@ -287,6 +296,8 @@ struct MimoArgs {
 extern "C" {
 int mpcq_internal_setup_launch(const mpcq::SetupArgs *args, hipStream_t stream);
 int mpcq_internal_setup_wave_launch(const mpcq::SetupArgs *args, hipStream_t stream);
+// Per-plant setup with the direct inverse M(rho)^-1 (mpcq_setup_wave.hip; n <= 32, m <= 64).
+int mpcq_internal_setup_inv_launch(const mpcq::SetupArgs *args, hipStream_t stream);
 size_t mpcq_internal_setup_wave_lds(int n, int m);
 int mpcq_internal_f64_to_f32(const double *in, float *out, size_t count, hipStream_t s);
 int mpcq_internal_broadcast(const double *src, double *dst, int len, int batch, int per_qp_src, hipStream_t s);

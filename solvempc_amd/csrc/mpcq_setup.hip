@@ -282,7 +282,10 @@ __global__ __launch_bounds__(64) void setup_kernel(SetupArgs a)
         }
         o_WtA[e] = b;
         o_Ah[e] = ah;
+        out[Lo.Bt + e] = b;  // eigen-basis: Bt = A^ W
     }
+    for (int e = t; e < nc * nc; e += T) out[Lo.G + e] = o_W[e];  // G = W (written above by this thread)
+    if (t == 0) out[Lo.rho0] = -1.0;
     __syncthreads();
     if (t == 0) {
         a.status[p] = fail ? kNonCvx : 0;

@@ -90,41 +90,15 @@ __device__ inline void circle_pair(int r, int u, int ne, int &p, int &q)
     else { p = (r + u) % k; q = (r - u + k) % k; }
 }
 
-__global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
+// OSQP scale_data (Ruiz equilibration + cost normalisation) and set_rho_vec's constraint typing, on
+// the LDS-resident plant (one wave).  On exit Ph, Ah hold P^, A^; Dv, Ev the scalings; Et the rho
+// scale of each row (0 free, 1 inequality, RHO_EQ_OVER_RHO_INEQ equality); returns c.
+__device__ double ruiz_and_types(const SetupArgs &a, int pl, int t, int n, int m, int mc, int ld, double *Ph,
+                                 double *Ah, double *Dv, double *Ev, double *Dt, double *Et, double *qh, double *sh,
+                                 int *ctype)
 {
-    extern __shared__ double sm[];
-    const int pl = blockIdx.x;
-    if (pl >= a.n_plants) return;
-    const int t = threadIdx.x;
-    const int n = a.n, m = a.m, nc = a.nc, mc = a.mc;
-    const SetupWaveShape S = SetupWaveShape::make(n, m);
-    const int ld = S.ld, ne = S.ne;
-    double *Ph = sm + S.Ph, *Ah = sm + S.Ah, *L = sm + S.L, *Tm = sm + S.T, *C = sm + S.C, *V = sm + S.V;
-    double *Dv = sm + S.Dv, *Ev = sm + S.Ev, *Dt = sm + S.Dt, *Et = sm + S.Et, *qh = sm + S.qh;
-    double *rot = sm + S.rot, *sh = sm + S.total - 8;
-
-    const double *P = a.P + (size_t)pl * n * n;
-    const double *q0 = a.q0 + (size_t)pl * n;
-    const double *A = a.A + (size_t)pl * m * n;
     const double *l0 = a.l0 + (size_t)pl * m;
     const double *u0 = a.u0 + (size_t)pl * m;
-    const OpsLayout Lo = OpsLayout::make(nc, mc);
-    double *out = a.ops + (size_t)pl * Lo.total;
-    int *ctype = a.ctype + (size_t)pl * mc;
-
-    MPCQ_STAMP(0);
-    // ---- data (osqp-eigen keeps the upper triangle of the Hessian)
-    for (int e = t; e < n * n; e += 64) {
-        const int i = e / n, j = e % n;
-        Ph[i * ld + j] = (i <= j) ? P[i * n + j] : P[j * n + i];
-    }
-    for (int e = t; e < m * n; e += 64) Ah[(e / n) * ld + e % n] = A[e];
-    for (int j = t; j < n; j += 64) { qh[j] = q0[j]; Dv[j] = 1.0; }
-    for (int i = t; i < m; i += 64) Ev[i] = 1.0;
-    if (t == 0) sh[0] = 1.0;
-    __syncthreads();
-
-    MPCQ_STAMP(1);
     // ---- Ruiz equilibration + cost normalisation (OSQP scale_data).  A pass's cost factor ct is not
     // swept over P^ on its own: it stays pending (cp) and is applied inside the next pass's column
     // norms (max |cp P| = cp max |P|: rounding is monotone) and D-scaling, or by one sweep after the
@@ -180,7 +154,6 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
     }
     const double cost = sh[0];
 
-    MPCQ_STAMP(2);
     // ---- constraint types from the scaled setup bounds (OSQP set_rho_vec); Et <- rscale
     for (int i = t; i < m; i += 64) {
         const double lo = l0[i] * Ev[i], up = u0[i] * Ev[i];
@@ -196,6 +169,43 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
     for (int i = m + t; i < mc; i += 64) ctype[i] = 0;
     __syncthreads();
 
+    return cost;
+}
+
+__global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
+{
+    extern __shared__ double sm[];
+    const int pl = blockIdx.x;
+    if (pl >= a.n_plants) return;
+    const int t = threadIdx.x;
+    const int n = a.n, m = a.m, nc = a.nc, mc = a.mc;
+    const SetupWaveShape S = SetupWaveShape::make(n, m);
+    const int ld = S.ld, ne = S.ne;
+    double *Ph = sm + S.Ph, *Ah = sm + S.Ah, *L = sm + S.L, *Tm = sm + S.T, *C = sm + S.C, *V = sm + S.V;
+    double *Dv = sm + S.Dv, *Ev = sm + S.Ev, *Dt = sm + S.Dt, *Et = sm + S.Et, *qh = sm + S.qh;
+    double *rot = sm + S.rot, *sh = sm + S.total - 8;
+
+    const double *P = a.P + (size_t)pl * n * n;
+    const double *q0 = a.q0 + (size_t)pl * n;
+    const double *A = a.A + (size_t)pl * m * n;
+    const OpsLayout Lo = OpsLayout::make(nc, mc);
+    double *out = a.ops + (size_t)pl * Lo.total;
+    int *ctype = a.ctype + (size_t)pl * mc;
+
+    MPCQ_STAMP(0);
+    // ---- data (osqp-eigen keeps the upper triangle of the Hessian)
+    for (int e = t; e < n * n; e += 64) {
+        const int i = e / n, j = e % n;
+        Ph[i * ld + j] = (i <= j) ? P[i * n + j] : P[j * n + i];
+    }
+    for (int e = t; e < m * n; e += 64) Ah[(e / n) * ld + e % n] = A[e];
+    for (int j = t; j < n; j += 64) { qh[j] = q0[j]; Dv[j] = 1.0; }
+    for (int i = t; i < m; i += 64) Ev[i] = 1.0;
+    if (t == 0) sh[0] = 1.0;
+    __syncthreads();
+
+    MPCQ_STAMP(1);
+    const double cost = ruiz_and_types(a, pl, t, n, m, mc, ld, Ph, Ah, Dv, Ev, Dt, Et, qh, sh, ctype);
     MPCQ_STAMP(3);
     // ---- P~ = P^ + sigma I + RHO_MIN sum_free a a' (into L), G = sum rscale a a' (into Tm)
     for (int e = t; e < n * n; e += 64) {
@@ -421,7 +431,10 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
         }
         o_WtA[e] = b;
         o_Ah[e] = ah;
+        out[Lo.Bt + e] = b;  // eigen-basis: Bt = A^ W, G = W
     }
+    for (int e = t; e < nc * nc; e += 64) out[Lo.G + e] = o_W[e];
+    if (t == 0) out[Lo.rho0] = -1.0;
     MPCQ_STAMP(8);
     if (t == 0) {
         a.status[pl] = fail ? kNonCvx : 0;
@@ -430,7 +443,146 @@ __global__ __launch_bounds__(64) void setup_wave_kernel(SetupArgs a)
     }
 }
 
+// In-place Gauss-Jordan inverse of an SPD matrix in LDS (n <= 32, row stride ld), 64 threads; no
+// pivoting (SPD: every pivot is positive).  Returns false when a pivot is not positive (P^ + sigma I
+// + rho A^'A^ not positive definite: OSQP's setup would fail to factor it).
+__device__ bool gj_invert_spd(double *M, int n, int ld, int t)
+{
+    bool ok = true;
+    for (int k = 0; k < n; k++) {
+        const double piv = M[k * ld + k];
+        if (!(piv > 0.0)) ok = false;
+        const double ip = 1.0 / piv;
+        double nv[16];  // this thread's elements t + 64 c (n*n <= 1024): static indices, registers
+#pragma unroll
+        for (int c = 0; c < 16; c++) {
+            const int e = t + 64 * c;
+            if (e < n * n) {
+                const int i = e / n, j = e % n;
+                double v;
+                if (i == k && j == k) v = ip;
+                else if (i == k) v = M[k * ld + j] * ip;
+                else if (j == k) v = -M[i * ld + k] * ip;
+                else v = M[i * ld + j] - M[i * ld + k] * (M[k * ld + j] * ip);
+                nv[c] = v;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < 16; c++) {
+            const int e = t + 64 * c;
+            if (e < n * n) M[(e / n) * ld + e % n] = nv[c];
+        }
+        __syncthreads();
+    }
+    return ok;
+}
+
+// Per-plant setup with the direct inverse (batches of distinct plants, BASELINE config 3): OSQP's
+// scale_data and set_rho_vec as setup_wave_kernel, then M(rho0) = P^ + sigma I + sum_j rho_j a_j a_j'
+// (rho_j = rho0 * rscale_j, RHO_MIN on free rows) and its inverse by Gauss-Jordan: O(n^3) in place
+// of the eigen-basis's Cholesky + Jacobi sweeps.  Writes the operator block in the direct-inverse
+// reading of OpsLayout (mpcq_internal.h): W = W^-1 = I, lambda = 0, sigma W'W = sigma M^-1,
+// G = M^-1, Bt = A^ M^-1, PW = P^, WtA = Ah = A^, rho0.
+__global__ __launch_bounds__(64) void setup_inv_kernel(SetupArgs a)
+{
+    extern __shared__ double sm[];
+    const int pl = blockIdx.x;
+    if (pl >= a.n_plants) return;
+    const int t = threadIdx.x;
+    const int n = a.n, m = a.m, nc = a.nc, mc = a.mc;
+    const SetupWaveShape S = SetupWaveShape::make(n, m);
+    const int ld = S.ld;
+    double *Ph = sm + S.Ph, *Ah = sm + S.Ah, *Mi = sm + S.L;
+    double *Dv = sm + S.Dv, *Ev = sm + S.Ev, *Dt = sm + S.Dt, *Et = sm + S.Et, *qh = sm + S.qh;
+    double *sh = sm + S.total - 8;
+    const double *P = a.P + (size_t)pl * n * n;
+    const double *q0 = a.q0 + (size_t)pl * n;
+    const double *A = a.A + (size_t)pl * m * n;
+    const OpsLayout Lo = OpsLayout::make(nc, mc);
+    double *out = a.ops + (size_t)pl * Lo.total;
+    int *ctype = a.ctype + (size_t)pl * mc;
+
+    MPCQ_STAMP(0);
+    for (int e = t; e < n * n; e += 64) {  // (osqp-eigen keeps the upper triangle of the Hessian)
+        const int i = e / n, j = e % n;
+        Ph[i * ld + j] = (i <= j) ? P[i * n + j] : P[j * n + i];
+    }
+    for (int e = t; e < m * n; e += 64) Ah[(e / n) * ld + e % n] = A[e];
+    for (int j = t; j < n; j += 64) { qh[j] = q0[j]; Dv[j] = 1.0; }
+    for (int i = t; i < m; i += 64) Ev[i] = 1.0;
+    if (t == 0) sh[0] = 1.0;
+    __syncthreads();
+    MPCQ_STAMP(1);
+    const double cost = ruiz_and_types(a, pl, t, n, m, mc, ld, Ph, Ah, Dv, Ev, Dt, Et, qh, sh, ctype);
+    MPCQ_STAMP(3);
+
+    // ---- M(rho0) and its inverse
+    const double rho = fmin(fmax(a.rho, kRhoMin), kRhoMax);
+    for (int e = t; e < n * n; e += 64) {
+        const int i = e / n, k = e % n;
+        double v = Ph[i * ld + k] + (i == k ? a.sigma : 0.0);
+        for (int r = 0; r < m; r++) {
+            const double rr = Et[r] == 0.0 ? kRhoMin : rho * Et[r];
+            v += rr * (Ah[r * ld + i] * Ah[r * ld + k]);
+        }
+        Mi[i * ld + k] = v;
+    }
+    __syncthreads();
+    const bool ok = gj_invert_spd(Mi, n, ld, t);
+    MPCQ_STAMP(6);
+
+    // ---- operator block (zero padded to nc x mc)
+    for (int e = t; e < nc * nc; e += 64) {
+        const int i = e / nc, k = e % nc;
+        const bool in = i < n && k < n;
+        const double mi = in ? Mi[i * ld + k] : 0.0, id = (i == k && i < n) ? 1.0 : 0.0;
+        out[Lo.W + e] = id;
+        out[Lo.Winv + e] = id;
+        out[Lo.sWtW + e] = a.sigma * mi;
+        out[Lo.G + e] = mi;
+        out[Lo.PW + e] = in ? Ph[i * ld + k] : 0.0;
+    }
+    for (int e = t; e < mc * nc; e += 64) {
+        const int j = e / nc, k = e % nc;
+        double ah = 0.0, bt = 0.0;
+        if (j < m && k < n) {
+            ah = Ah[j * ld + k];
+            for (int r = 0; r < n; r++) bt += Ah[j * ld + r] * Mi[r * ld + k];
+        }
+        out[Lo.WtA + e] = ah;
+        out[Lo.Ah + e] = ah;
+        out[Lo.Bt + e] = bt;
+    }
+    for (int k = t; k < nc; k += 64) {
+        out[Lo.lam + k] = 0.0;
+        out[Lo.D + k] = k < n ? Dv[k] : 1.0;
+        out[Lo.Dinv + k] = k < n ? 1.0 / Dv[k] : 1.0;
+    }
+    for (int i = t; i < mc; i += 64) {
+        out[Lo.E + i] = i < m ? Ev[i] : 1.0;
+        out[Lo.Einv + i] = i < m ? 1.0 / Ev[i] : 1.0;
+        out[Lo.rscale + i] = i < m ? Et[i] : 1.0;
+    }
+    if (t == 0) {
+        out[Lo.cs] = cost;
+        out[Lo.cs + 1] = 1.0 / cost;
+        out[Lo.rho0] = rho;
+        a.status[pl] = ok ? 0 : kNonCvx;
+        if (!ok) atomicOr(a.flags, 1);
+    }
+    MPCQ_STAMP(8);
+}
+
 }  // namespace mpcq
+
+extern "C" int mpcq_internal_setup_inv_launch(const mpcq::SetupArgs *args, hipStream_t stream)
+{
+    if (args->n < 1 || args->n > 32 || args->m > 64) return -1;
+    const size_t lds = 8 * mpcq::SetupWaveShape::make(args->n, args->m).total;
+    hipLaunchKernelGGL(mpcq::setup_inv_kernel, dim3(args->n_plants), dim3(64), lds, stream, *args);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
 
 extern "C" size_t mpcq_internal_setup_wave_lds(int n, int m)
 {

@@ -89,8 +89,55 @@ __device__ __forceinline__ T mem_dot(const T *M, size_t stride, const T *bc, T a
     return acc;
 }
 
+// Direct-inverse operators (mpcq_internal.h) for a rho other than the one they were built for:
+// M = P^ + sigma I + sum_j rho_j a_j a_j' (fp64 in LDS, stride NCAP + 1) and its Gauss-Jordan inverse
+// in place (SPD: no pivoting).  OSQP refactors its KKT matrix at the same points.  (Out of line and
+// free of the caller's register arrays: the operator rows are reloaded from `mi` by the caller.)
+template <typename T, int NCAP>
+__device__ __noinline__ void build_minv(const T *ops, const int *ctype, const OpsLayout &L, int n, int m, int nc,
+                                        double sigma, double rho, double *mi)
+{
+    constexpr int LD = NCAP + 1, PER = (NCAP * NCAP + 63) / 64;
+    const int lane = threadIdx.x;
+    __syncthreads();
+    for (int e = lane; e < n * n; e += 64) {
+        const int i = e / n, k = e % n;
+        double v = (double)ops[L.PW + (size_t)i * nc + k] + (i == k ? sigma : 0.0);
+        for (int r = 0; r < m; r++) {
+            const double rj = ctype[r] == -1 ? kRhoMin : rho * (double)ops[L.rscale + r];
+            v += rj * ((double)ops[L.WtA + (size_t)r * nc + i] * (double)ops[L.WtA + (size_t)r * nc + k]);
+        }
+        mi[i * LD + k] = v;
+    }
+    __syncthreads();
+    for (int k = 0; k < n; k++) {
+        const double ip = 1.0 / mi[k * LD + k];
+        double nv[PER];
+#pragma unroll
+        for (int c = 0; c < PER; c++) {
+            const int e = lane + 64 * c;
+            if (e < n * n) {
+                const int i = e / n, j = e % n;
+                double v;
+                if (i == k && j == k) v = ip;
+                else if (i == k) v = mi[k * LD + j] * ip;
+                else if (j == k) v = -mi[i * LD + k] * ip;
+                else v = mi[i * LD + j] - mi[i * LD + k] * (mi[k * LD + j] * ip);
+                nv[c] = v;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < PER; c++) {
+            const int e = lane + 64 * c;
+            if (e < n * n) mi[(e / n) * LD + e % n] = nv[c];
+        }
+        __syncthreads();
+    }
+}
+
 template <typename T, int NCAP, int MCAP, bool ALL_INEQ, bool LFREE>
-__device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int mc, int b, T *bcx, T *bcw)
+__device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int mc, int b, T *bcx, T *bcw, double *mi)
 {
     constexpr int VEC = 16 / sizeof(T);
     constexpr int BN = (NCAP + VEC - 1) / VEC * VEC, BM = (MCAP + VEC - 1) / VEC * VEC;
@@ -114,7 +161,7 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
 #pragma unroll
     for (int i = 0; i < NCAP; i++) Srow[i] = ops[L.sWtW + (size_t)kl * nc + i];
 #pragma unroll
-    for (int j = 0; j < MCAP; j++) Btrow[j] = ops[L.WtA + (size_t)j * nc + kl];
+    for (int j = 0; j < MCAP; j++) Btrow[j] = ops[L.Bt + (size_t)j * nc + kl];
 #pragma unroll
     for (int k = 0; k < NCAP; k++) Brow[k] = ops[L.WtA + (size_t)jl * nc + k];
     for (int i = lane; i < BN; i += 64) bcx[i] = T(0);
@@ -179,14 +226,16 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
     }
     int status = wor(bad) ? kInvalidBounds : (wor(tchg) ? kTypeChanged : kUnsolved);
 
-    // g = W' q^ (lane k: column k of W)
+    // g = G' q^ (lane k: column k of G = W, or of M^-1 for direct-inverse operators)
     if (ln) bcx[lane] = qh;
     wave_sync();
     T gk = T(0);
     {
-        gk = mem_dot<T, NCAP>(ops + L.W + kl, nc, bcx, gk);
+        gk = mem_dot<T, NCAP>(ops + L.G + kl, nc, bcx, gk);
     }
     gk = ln ? -gk : T(0);
+    const T rho0 = ops[L.rho0];  // direct-inverse operators: the rho they hold (eigen basis: -1)
+    const bool inv = rho0 > T(0);
 
     // ---- state
     T xs = T(0), z = T(0), y = T(0), rho;
@@ -207,6 +256,25 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
         }
     }
     it = __builtin_amdgcn_readfirstlane(it);
+    // direct-inverse operators for the QP's rho: sigma M^-1 (row k), (A^ M^-1)' (row k), g = -M^-1 q^
+    // (q^ in bcx), from M(rho)^-1 rebuilt in `mi`
+    auto reload_rows = [&]() {
+        constexpr int LD = NCAP + 1;
+#pragma unroll
+        for (int i = 0; i < NCAP; i++) Srow[i] = (i < n) ? (T)(st.sigma * mi[kl * LD + i]) : T(0);
+#pragma unroll
+        for (int j = 0; j < MCAP; j++) {
+            double v = 0.0;
+            if (j < m)
+                for (int r = 0; r < n; r++) v += (double)ops[L.WtA + (size_t)j * nc + r] * mi[r * LD + kl];
+            Btrow[j] = (T)v;
+        }
+        double g = 0.0;
+        for (int i = 0; i < n; i++) g += mi[i * LD + kl] * (double)bcx[i];
+        gk = ln ? (T)(-g) : T(0);
+        __syncthreads();
+    };
+    bool refactor = inv && rho != rho0;  // done at the top of the next iteration (one code site)
     T rinv = T(1) / rho;
     const T lamk = ln ? ops[L.lam + lane] : T(0);
     T dk = T(1) / (T(1) + rho * lamk);
@@ -265,6 +333,14 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
 #define MPCQ_WSTAMP(k) do { } while (0)
 #endif
     for (;;) {
+        if (refactor) {  // (cold) OSQP's KKT refactorisation after a rho change
+            wave_sync();
+            if (ln) bcx[lane] = qh;
+            wave_sync();
+            build_minv<T, NCAP>(ops, ctype, L, n, m, nc, st.sigma, (double)rho, mi);
+            reload_rows();
+            refactor = false;
+        }
         it++;
         MPCQ_WSTAMP(0);
         const bool at_check = it == next_check;
@@ -434,6 +510,7 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
                 rho = tt_min(tt_max(rn, T(kRhoMin)), T(kRhoMax));
                 rinv = T(1) / rho;
                 dk = T(1) / (T(1) + rho * lamk);
+                refactor = inv;  // direct inverse: M(rho)^-1 and the operator rows built on it
             }
         }
         if (!term && last) {
@@ -476,6 +553,7 @@ __global__ __launch_bounds__(64, 2) void admm_wave_kernel(AdmmArgs<T> a, int nc,
     constexpr int BN = (NCAP + VEC - 1) / VEC * VEC, BM = (MCAP + VEC - 1) / VEC * VEC;
     __shared__ __attribute__((aligned(16))) T bcx[BN];  // x'-side broadcast (x', eta, q^, dx)
     __shared__ __attribute__((aligned(16))) T bcw[BM];  // row-side broadcast (w, y, d)
+    __shared__ double mi[NCAP * (NCAP + 1)];            // direct-inverse refactorisation (cold path)
     if (blockIdx.x == 0 && threadIdx.x < ListSeg::kShards) {  // counters no launch of this chain is using
         if (a.zero_cnt) a.zero_cnt[threadIdx.x * ListSeg::kStride] = 0;
         if (a.zero_cnt0) a.zero_cnt0[threadIdx.x * ListSeg::kStride] = 0;
@@ -484,11 +562,11 @@ __global__ __launch_bounds__(64, 2) void admm_wave_kernel(AdmmArgs<T> a, int nc,
         const int sg = blockIdx.x % ListSeg::kShards, per = gridDim.x / ListSeg::kShards;
         const int count = a.count_in[sg * ListSeg::kStride];
         for (int slot = blockIdx.x / ListSeg::kShards; slot < count; slot += per)  // uniform: one wave per block
-            wave_solve_one<T, NCAP, MCAP, ALL_INEQ, LFREE>(a, nc, mc, a.list_in[sg * a.list_seg + slot], bcx, bcw);
+            wave_solve_one<T, NCAP, MCAP, ALL_INEQ, LFREE>(a, nc, mc, a.list_in[sg * a.list_seg + slot], bcx, bcw, mi);
         return;
     }
     for (int slot = blockIdx.x; slot < a.batch; slot += gridDim.x)  // uniform: one wave per block
-        wave_solve_one<T, NCAP, MCAP, ALL_INEQ, LFREE>(a, nc, mc, a.qp0 + slot, bcx, bcw);
+        wave_solve_one<T, NCAP, MCAP, ALL_INEQ, LFREE>(a, nc, mc, a.qp0 + slot, bcx, bcw, mi);
 }
 
 

@@ -508,11 +508,12 @@ def test_stream_workload_stays_solved_and_bounded(plant):
 
 
 @pytest.mark.parametrize("n,m", [(5, 7), (13, 30), (20, 40), (32, 64)])
-def test_setup_wave_vs_workgroup_kernel(n, m):
-    """Per-plant setup, one wave per plant with the parallel-ordering Jacobi (mpcq_setup_wave.hip),
-    against the serial workgroup kernel (MPCQ_SETUP=ref) and the oracle: identical Ruiz scaling, the
-    oracle's status / iteration count and |dx| <= 1e-8 on random convex QPs of odd and even order
-    (equality rows, finite and free lower bounds)."""
+def test_per_plant_setups_agree(n, m):
+    """Per-plant setup three ways on random convex QPs of odd and even order (equality rows, finite
+    and free lower bounds): the direct inverse of M(rho) (the default for per-plant batches,
+    setup_inv_kernel, with the wave kernel's in-kernel refactorisation when rho adapts), the wave
+    kernel's eigen-basis (MPCQ_SETUP=eigen) and the serial workgroup kernel (MPCQ_SETUP=ref): the same
+    Ruiz scaling bit for bit, and the oracle's status / iteration count and |dx| <= 1e-8 for each."""
     rng = np.random.default_rng(n * 100 + m)
     B = 24
     Ps, As, ls, us, qs = [], [], [], [], []
@@ -527,8 +528,9 @@ def test_setup_wave_vs_workgroup_kernel(n, m):
         ls.append(lo); us.append(up); qs.append(rng.normal(size=n))
     P, A, l, u, q = map(np.stack, (Ps, As, ls, us, qs))
     out = {}
-    for mode in ("ref", "wave"):
-        os.environ["MPCQ_SETUP"] = mode
+    for mode in ("ref", "eigen", "inv"):
+        if mode != "inv":
+            os.environ["MPCQ_SETUP"] = mode
         try:
             s = sm.BatchSolver(n, m, B, n_plants=B)
             s.setup(P, np.zeros((B, n)), A, l, u)
@@ -537,15 +539,46 @@ def test_setup_wave_vs_workgroup_kernel(n, m):
         s.update_lin_cost(q)
         s.solve()
         out[mode] = (s.solution(), *s.info(), s.scaling())
-    xr, str_, itr, _, scr = out["ref"]
-    xw, stw, itw, _, scw = out["wave"]
-    for a_, b_ in zip(scr, scw):
-        assert np.array_equal(np.asarray(a_), np.asarray(b_))
-    for b in range(B):
-        x_o, st_o, it_o, _ = oracle.batch_solve(P[b], A[b], np.zeros(n), l[b], u[b], q[b][None], u[b][None])
-        assert stw[b] == st_o[0] and itw[b] == it_o[0], b
-        assert np.abs(xw[b] - x_o[0]).max() < 1e-8
-    assert np.array_equal(stw, str_) and np.abs(xw - xr).max() < 1e-8
+    ref = [oracle.batch_solve(P[b], A[b], np.zeros(n), l[b], u[b], q[b][None], u[b][None]) for b in range(B)]
+    for mode, (x, st, it, rho, sc) in out.items():
+        for a_, b_ in zip(out["ref"][4], sc):
+            assert np.array_equal(np.asarray(a_), np.asarray(b_)), mode
+        for b in range(B):
+            x_o, st_o, it_o, rho_o = ref[b]
+            assert st[b] == st_o[0] and it[b] == it_o[0], (mode, b)
+            assert abs(rho[b] - rho_o[0]) <= 1e-9 * rho_o[0], (mode, b)
+            assert np.abs(x[b] - x_o[0]).max() < 1e-8, (mode, b)
+
+
+def test_direct_inverse_refactors_on_rho_change(plant):
+    """A per-plant batch whose rho adapts (OSQP adapt_rho at iteration 100): the direct-inverse path
+    rebuilds M(rho)^-1 in the kernel and stays on the oracle's trajectory; a warm-started second solve
+    starts from the adapted rho (operators rebuilt in the prologue) and matches too."""
+    N, B = 20, 64
+    ops = oracle.condense(plant, N)
+    X, U = workload.mpc_states(13, 0, B, u_range=3.0)
+    q, u = oracle.gradient(ops, X, U), oracle.upper_bound(ops, X, U)
+    l = np.full(2 * N, LMIN)
+    u0 = oracle.upper_bound(ops, np.zeros(4), 0.0)
+    s = sm.BatchSolver(N, 2 * N, B, n_plants=B)
+    s.setup(np.tile(ops["P"], (B, 1, 1)), np.zeros((B, N)), np.tile(ops["A"], (B, 1, 1)), np.tile(l, (B, 1)),
+            np.tile(u0, (B, 1)))
+    refs = [oracle.Solver(ops["P"], np.zeros(N), ops["A"], l, u0) for _ in range(B)]
+    moved = 0
+    for rnd in range(2):
+        s.update_lin_cost(q)
+        s.update_upper_bound(u)
+        s.solve()
+        x = s.solution()
+        st, it, rho = s.info()
+        for b, r in enumerate(refs):
+            assert r.update_gradient(q[b]) and r.update_upper_bound(u[b])
+            r.solve()
+            assert st[b] == r.info().status and it[b] == r.info().iter, (rnd, b)
+            assert abs(rho[b] - r.info().rho) <= 1e-9 * r.info().rho
+            np.testing.assert_allclose(x[b], r.x(), rtol=0, atol=1e-9)
+        moved += int(np.sum(rho != 0.1))
+    assert moved > 0, "no QP adapted rho: the refactorisation path was not exercised"
 
 
 def _perturbed_plants(plant, B, seed):
