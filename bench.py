@@ -420,7 +420,6 @@ def main_lti(a, rank, world, local, dist, dev):
         stream, sptr = side, side.cuda_stream
         X0_d = X_d.clone()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
-    ev_mid = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
     cur = torch.cuda.current_stream(dev)
 
     def step(i=None):
@@ -436,11 +435,11 @@ def main_lti(a, rank, world, local, dist, dev):
             solver.mpc_run_device(X_d.data_ptr(), U_d.data_ptr(), plant["xref"], a.ctrl_steps, a.seed, start, 0,
                                   a.noise, sptr)
         else:
-            if perplant:  # condensing + Ruiz + KKT setup of every plant, on the device
-                solver.mpc_setup_plants_device(4, 10, *[t.data_ptr() for t in plant_d], sptr)
-                if i is not None:
-                    ev_mid[i].record(stream)  # setup | solve boundary (same stream)
-            solver.mpc_step_device(X_d.data_ptr(), U_d.data_ptr(), plant["xref"], sptr)
+            if perplant:  # every plant's ctor + controllerStep in one pass, operators on chip
+                solver.mpc_plants_step_device(4, 10, *[t.data_ptr() for t in plant_d], X_d.data_ptr(),
+                                              U_d.data_ptr(), plant["xref"], sptr)
+            else:
+                solver.mpc_step_device(X_d.data_ptr(), U_d.data_ptr(), plant["xref"], sptr)
         if i is not None:
             ev[i][1].record(stream)
         if stream_mode:
@@ -449,11 +448,8 @@ def main_lti(a, rank, world, local, dist, dev):
 
     wall, got = _timed_loop(a, step, dist, world, dev)
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
-    if perplant:
-        setup_ms = float(np.mean([s.elapsed_time(m_) for (s, _), m_ in zip(ev, ev_mid)]))
-        solve_ms = float(np.mean([m_.elapsed_time(e) for (_, e), m_ in zip(ev, ev_mid)]))
 
-    status, iters, _ = solver.info()
+    status, iters, rho_f = solver.info()
     kind, paired = solver.path()
     qps_per_step = B * (a.ctrl_steps if stream_mode else 1)
     if stream_mode:  # iterations every QP ran over all control steps of the last bench step (device counters)
@@ -501,23 +497,23 @@ def main_lti(a, rank, world, local, dist, dev):
         rec["iters"]["final_max_abs_X"] = float(X_d.abs().max().item())
     rec["collective"] = _collective(dist, world, got)
     if perplant:
-        # The step is two stages of different character: per-plant condensing + setup (fp64 VALU/LDS,
-        # one wave per plant) and the one-QP-per-wave ADMM solve (VALU, T = dtype).  Each is priced
-        # against its own vector peak; the timed span of the setup stage includes the host read-back
-        # of the setup status word (mpcq_mpc_setup_plants_device synchronises once).
-        setup_flops = B * workload.flops_plant_setup(N, 2 * N)
-        rec["roofline"] = {"bound": "valu", "achieved": setup_flops / (setup_ms * 1e-3) / 1e12,
-                           "peak": PEAK_TFLOPS["f64"], "unit": "TFLOP/s",
-                           "frac": setup_flops / (setup_ms * 1e-3) / 1e12 / PEAK_TFLOPS["f64"], "traffic": None,
-                           "kernel": "condense_wave_kernel + setup_wave_kernel (fp64 vector peak)",
-                           "kernel_ms": setup_ms, "flops_per_step": setup_flops,
-                           "flops_note": "algorithmic per plant (SURVEY §8d): F_condense + Ruiz + one LDL of the "
-                                         "KKT system"}
-        rec["stages"] = {"setup_ms": setup_ms, "solve_ms": solve_ms, "step_ms": kern_ms,
-                         "solve_roofline": {"bound": "valu", "achieved": flops / (solve_ms * 1e-3) / 1e12,
-                                            "peak": PEAK_TFLOPS[a.dtype], "unit": "TFLOP/s",
-                                            "frac": flops / (solve_ms * 1e-3) / 1e12 / PEAK_TFLOPS[a.dtype],
-                                            "kernel": "admm_wave_kernel", "flops_per_step": flops}}
+        # One kernel per step: condensing + Ruiz + KKT inverse (fp64) and the ADMM (T = dtype) of every
+        # plant, two plants per wave.  FLOPs as the kernel performs them (workload.flops_plant_step;
+        # a refactorisation per plant whose rho moved), priced at the vector peak of the ADMM's type.
+        rho0 = solver.settings.rho if a.dtype == "f64" else float(np.float32(solver.settings.rho))
+        refac = (rho_f != rho0).astype(np.float64)
+        pf = float(workload.flops_plant_step(N, 4, iters, refac, solver.settings.scaling).sum())
+        ach = pf / (kern_ms * 1e-3) / 1e12
+        rec["roofline"] = {"bound": "valu", "achieved": ach, "peak": PEAK_TFLOPS[a.dtype], "unit": "TFLOP/s",
+                           "frac": ach / PEAK_TFLOPS[a.dtype], "traffic": None,
+                           "kernel": "plant_step_kernel (condense + setup + solve, one pass)", "kernel_ms": kern_ms,
+                           "flops_per_step": pf,
+                           "flops_note": "as performed (workload.flops_plant_step): condensing, Ruiz, 8N^3 per KKT "
+                                         "inverse (setup + one per rho change), 6N^2 + 20N per iteration (paired "
+                                         "rows), 6N^2 + 30N per check; the fp64 setup is priced at the same peak",
+                           "dense_equivalent": {"flops_per_step": flops_dense + B * workload.flops_plant_setup(N, 2 * N),
+                                                "note": "SURVEY §8d: dense F_iter / F_check + F_condense + Ruiz + one LDL"}}
+        rec["iters"]["rho_adapted_frac"] = float(refac.mean())
     if a.cpu_seconds > 0 and not stream_mode:
         import oracle
 

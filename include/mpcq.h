@@ -198,6 +198,19 @@ int mpcq_mpc_setup_plants_device(mpcq_ctx *ctx, int nx, int s_rows, const double
                                  const double *Bd, const double *Cd, const double *K,
                                  const double *Q, const double *R, const double *RD, void *stream);
 
+/* Per-plant batch in one pass (BASELINE config 3): for every plant the reference's constructor
+ * (condensing + osqp_setup on the ctor's data, X = U = 0: :3-65) and one controllerStep (:81-108) from
+ * device-resident X (batch*nx) and U (batch; U += x[0] when SOLVED) — the work of
+ * mpcq_mpc_setup_plants_device followed by mpcq_mpc_step_device, with each plant's operators kept on
+ * chip instead of written to the context.  Plant arrays as in mpcq_mpc_setup_plants_device.
+ * Afterwards the context holds this step's solution, dual, status, iterations and rho; it holds no
+ * operators, so further solves need mpcq_mpc_setup_plants_device / mpcq_setup first (MPCQ_ERR_ORDER
+ * otherwise).  Asynchronous on `stream`; a plant whose KKT matrix is not positive definite ends
+ * MPCQ_NON_CVX.  Needs n == N <= 32, m == 2N, n_plants == batch, nx <= 8. */
+int mpcq_mpc_plants_step_device(mpcq_ctx *ctx, int nx, int s_rows, const double *Ad, const double *Bd,
+                                const double *Cd, const double *K, const double *Q, const double *R,
+                                const double *RD, const double *X, double *U, double xref, void *stream);
+
 /* ---- MIMO condensed MPC (BASELINE config 4: quad-rotor hover linearisations, n_x 12, n_u 4, N 30) --
  * The reference's condensing (ModelPredictiveControlAPI.cpp:158-369) with every SISO scalar a block
  * (oracle/mpc_mimo.h): decision du in R^(N n_u), A = [L (x) K0; -(L (x) K0)], u = W0 + Sbar X + Ku U,

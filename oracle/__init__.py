@@ -115,7 +115,7 @@ def lib() -> C.CDLL:
     L.ora_matpow.argtypes = [C.c_int, dp, C.c_int, dp]
     L.ora_plants_step.restype = C.c_int
     L.ora_plants_step.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, dp, dp, dp, dp, C.c_double, C.c_double,
-                                  C.c_double, dp, dp, C.c_double, C.POINTER(Settings), dp, ip, ip, C.c_int]
+                                  C.c_double, dp, dp, C.c_double, C.POINTER(Settings), dp, ip, ip, C.c_int, dp, dp]
     L.ora_condense_mimo.restype = C.c_int
     L.ora_condense_mimo.argtypes = [C.POINTER(_MimoPlant), C.POINTER(_MimoOps)]
     L.ora_mimo_plants_step.restype = C.c_int
@@ -339,9 +339,10 @@ def batch_solve(P, A, q0, l, u0, q, u, settings: Settings | None = None, nthread
 
 
 def plants_step(plant: dict, Ad, Bd, X, U, N: int, s_rows: int = 10, xref: float = 0.0,
-                settings: Settings | None = None, nthreads: int = 0):
+                settings: Settings | None = None, nthreads: int = 0, full: bool = False):
     """Per-plant batch (config 3): for plant p with its own Ad[p], Bd[p] (Cd, K, Q, R, RD shared),
-    the reference constructor + one controllerStep from (X[p], U[p]).  Returns (U_new, status, iter)."""
+    the reference constructor + one controllerStep from (X[p], U[p]).  Returns (U_new, status, iter),
+    and with ``full`` also the solutions x (k, N) and the decision margins (Info.margin)."""
     Ad, Bd, X, U = _c64(Ad), _c64(Bd), _c64(X), _c64(U)
     k, nx = Ad.shape[0], Ad.shape[1]
     Cd, K = _c64(plant["Cd"]), _c64(plant["K"])
@@ -349,10 +350,12 @@ def plants_step(plant: dict, Ad, Bd, X, U, N: int, s_rows: int = 10, xref: float
     U_out = np.zeros(k)
     st = np.zeros(k, dtype=np.int32)
     it = np.zeros(k, dtype=np.int32)
+    x = np.zeros((k, N))
+    mg = np.zeros(k)
     lib().ora_plants_step(k, nx, N, s_rows, _dp(Ad), _dp(Bd), _dp(Cd), _dp(K), plant["Q"], plant["R"],
                           plant["RD"], _dp(X), _dp(U), float(xref), C.byref(s), _dp(U_out), _ip(st), _ip(it),
-                          nthreads)
-    return U_out, st, it
+                          nthreads, _dp(x), _dp(mg))
+    return (U_out, st, it, x, mg) if full else (U_out, st, it)
 
 
 def kkt_residuals(P, q, A, l, u, x, y) -> dict:

@@ -18,7 +18,7 @@
 int ora_plants_step(int n_plants, int nx, int N, int s_rows, const double *Ad, const double *Bd,
                     const double *Cd, const double *K, double Q, double R, double RD, const double *X,
                     const double *U, double xref, const ora_settings *s, double *U_out, int *status,
-                    int *iters, int nthreads)
+                    int *iters, int nthreads, double *x_out, double *margin)
 {
     int failed = 0;
 #ifdef _OPENMP
@@ -57,6 +57,9 @@ int ora_plants_step(int n_plants, int nx, int N, int s_rows, const double *Ad, c
             ora_get_info(w, &info);
             status[p] = info.status;
             iters[p] = info.iter;
+            if (margin) margin[p] = info.margin;
+            if (x_out)
+                for (int j = 0; j < n; j++) x_out[(size_t)p * n + j] = ora_solution_x(w)[j];
             if (info.status == ORA_SOLVED) U_out[p] = U[p] + ora_solution_x(w)[0];
             ora_cleanup(w);
         }

@@ -16,7 +16,7 @@ extern "C" {
 int ora_plants_step(int n_plants, int nx, int N, int s_rows, const double *Ad, const double *Bd,
                     const double *Cd, const double *K, double Q, double R, double RD, const double *X,
                     const double *U, double xref, const ora_settings *s, double *U_out, int *status,
-                    int *iters, int nthreads);
+                    int *iters, int nthreads, double *x_out, double *margin);
 
 #ifdef __cplusplus
 }

@@ -222,6 +222,15 @@ class BatchSolver:
                                                        C.c_void_p(stream or 0)), "mpcq_mpc_setup_plants_device")
         self.nx = int(nx)
 
+    def mpc_plants_step_device(self, nx: int, s_rows: int, Ad_ptr: int, Bd_ptr: int, Cd_ptr: int, K_ptr: int,
+                               Q_ptr: int, R_ptr: int, RD_ptr: int, X_ptr: int, U_ptr: int, xref: float = 0.0,
+                               stream: int | None = None) -> None:
+        """BASELINE config 3 in one pass: every plant's condensing + setup + one controllerStep (device
+        pointers, plant-major fp64), operators kept on chip (the context keeps results only)."""
+        ptrs = [C.c_void_p(p) for p in (Ad_ptr, Bd_ptr, Cd_ptr, K_ptr, Q_ptr, R_ptr, RD_ptr, X_ptr, U_ptr)]
+        _capi.check(lib().mpcq_mpc_plants_step_device(self._ctx, int(nx), int(s_rows), *ptrs, float(xref),
+                                                      C.c_void_p(stream or 0)), "mpcq_mpc_plants_step_device")
+
     # -- MIMO condensed MPC (BASELINE config 4; oracle/mpc_mimo.h formulation)
     def mimo_setup_plants_device(self, nx: int, nu: int, ny: int, s_rows: int, Ad_ptr: int, Bd_ptr: int, Cd_ptr: int,
                                  Q_ptr: int, R_ptr: int, RD_ptr: int, K_ptr: int, K0_ptr: int, w0_ptr: int,

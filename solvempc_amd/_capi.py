@@ -20,6 +20,7 @@ EXPORTS = (
     "mpcq_mpc_step", "mpcq_mpc_set_plant", "mpcq_mpc_simulate_device", "mpcq_mpc_run_device",
     "mpcq_condense", "mpcq_mpc_setup_plants_device", "mpcq_last_error", "mpcq_get_path",
     "mpcq_mimo_setup_plants_device", "mpcq_mimo_step_device", "mpcq_mpc_stream_counters",
+    "mpcq_mpc_plants_step_device",
 )
 
 
@@ -97,6 +98,7 @@ def lib() -> C.CDLL:
         "mpcq_mpc_run_device": (C.c_int, [vp, vp, vp, C.c_double, C.c_int, C.c_ulonglong, C.c_longlong,
                                           C.c_longlong, C.c_double, vp]),
         "mpcq_mpc_stream_counters": (C.c_int, [vp, ip, ip]),
+        "mpcq_mpc_plants_step_device": (C.c_int, [vp, C.c_int, C.c_int] + [vp] * 9 + [C.c_double, vp]),
         "mpcq_condense": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int] + [dp] * 15),
         "mpcq_mpc_setup_plants_device": (C.c_int, [vp, C.c_int, C.c_int] + [vp] * 7 + [vp]),
         "mpcq_last_error": (C.c_char_p, []),

@@ -75,7 +75,8 @@ struct mpcq_ctx {
     // The formulation the context was last set up for: the generic / condensed-MPC operators
     // (mpcq_setup, mpcq_mpc_setup_plants_device) or the MIMO operator blocks
     // (mpcq_mimo_setup_plants_device).  Each entry point checks for the one it runs on.
-    enum class Mode { None, Generic, Mimo } mode = Mode::None;
+    // OneShot: mpcq_mpc_plants_step_device left this step's results but no operators behind.
+    enum class Mode { None, Generic, Mimo, OneShot } mode = Mode::None;
     bool all_ineq = true, mpc_ready = false, lower_free = false, fresh = false;
     bool paired = false;  // shared plant of the condensed-MPC shape (tile kernel's paired loop)
     bool inv_ops = false; // per-plant operators in the direct-inverse reading (setup_inv_kernel): wave kernel only
@@ -257,6 +258,8 @@ int check_ctx(mpcq_ctx *c, Need need)
     if (need == kGeneric && c->mode != mpcq_ctx::Mode::Generic)
         return fail(MPCQ_ERR_ORDER, c->mode == mpcq_ctx::Mode::Mimo
                                         ? "the context was last set up by mpcq_mimo_setup_plants_device (MIMO)"
+                                    : c->mode == mpcq_ctx::Mode::OneShot
+                                        ? "mpcq_mpc_plants_step_device keeps no operators: set the plants up again"
                                         : "mpcq_setup has not succeeded");
     if (need == kAnySetup && c->mode == mpcq_ctx::Mode::None) return fail(MPCQ_ERR_ORDER, "no setup has succeeded");
     HIPCHK(hipSetDevice(c->dims.device));
@@ -1145,6 +1148,37 @@ int mpcq_mpc_setup_plants_device(mpcq_ctx *c, int nx, int s_rows, const double *
     return MPCQ_OK;
 }
 
+
+int mpcq_mpc_plants_step_device(mpcq_ctx *c, int nx, int s_rows, const double *Ad, const double *Bd,
+                                const double *Cd, const double *K, const double *Q, const double *R,
+                                const double *RD, const double *X, double *U, double xref, void *stream)
+{
+    int rc = check_generic_dims(c);
+    if (rc) return rc;
+    const int n = c->dims.n, m = c->dims.m;
+    if (nx <= 0 || nx > 8 || s_rows < 0) return fail(MPCQ_ERR_ARG, "plants_step: 1 <= nx <= 8, s_rows >= 0");
+    if (m != 2 * n || n > 32) return fail(MPCQ_ERR_ARG, "plants_step: n = N <= 32, m = 2N (ModelPredictiveControlAPI.cpp:47-48)");
+    if (c->dims.n_plants != c->dims.batch) return fail(MPCQ_ERR_ARG, "plants_step: one plant per QP (n_plants == batch)");
+    if (!Ad || !Bd || !Cd || !K || !Q || !R || !RD || !X || !U) return fail(MPCQ_ERR_ARG, "plants_step: null array");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipMemsetAsync(c->d_flags, 0, 4, s));
+    mpcq::PlantStepArgs a{};
+    a.n_plants = c->dims.batch;
+    a.nx = nx; a.N = n; a.s_rows = s_rows;
+    a.Ad = Ad; a.Bd = Bd; a.Cd = Cd; a.K = K; a.Q = Q; a.R = R; a.RD = RD;
+    a.X = X; a.U = U; a.xref = xref;
+    a.st = to_solver(c->set);
+    const int ct = c->set.check_termination;
+    a.adaptive_interval = c->set.adaptive_rho_interval ? c->set.adaptive_rho_interval : (ct ? 4 * ct : 100);
+    a.x = c->d_x; a.y = c->d_y; a.rho_out = c->d_rho; a.status = c->d_status; a.iter = c->d_iter;
+    a.flags = c->d_flags;
+    const int lr = mpcq_internal_plant_step_launch(&a, c->dims.dtype == MPCQ_F32, s);
+    if (lr) return fail(lr == -1 ? MPCQ_ERR_ARG : MPCQ_ERR_HIP, "plants_step kernel launch failed");
+    c->mode = mpcq_ctx::Mode::OneShot;  // results only: no operator blocks were written
+    c->mpc_ready = false;
+    c->last = s;
+    return MPCQ_OK;
+}
 
 int mpcq_mimo_setup_plants_device(mpcq_ctx *c, int nx, int nu, int ny, int s_rows, const double *Ad, const double *Bd,
                                   const double *Cd, const double *Q, const double *R, const double *RD, const double *K,

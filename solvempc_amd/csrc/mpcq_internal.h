@@ -292,6 +292,22 @@ struct MimoArgs {
 };
 }  // namespace mpcq
 
+namespace mpcq {
+// Arguments of plant_step_kernel (mpcq_plant.hip): condensing + setup + one controllerStep per SISO plant.
+struct PlantStepArgs {
+    int n_plants, nx, N, s_rows;
+    const double *Ad, *Bd, *Cd, *K, *Q, *R, *RD;  // [plant] nx*nx, nx, nx, nx, 1, 1, 1
+    const double *X;                               // [plant] nx (device)
+    double *U;                                     // [plant]    (device): U += x0 when solved
+    double xref;
+    SolverSettings st;
+    int adaptive_interval;
+    double *x, *y, *rho_out;                       // [plant] n, 2n unscaled solution; final rho
+    int *status, *iter;
+    int *flags;                                    // OR: 1 a plant's KKT matrix is not positive definite
+};
+}  // namespace mpcq
+
 // Launchers (extern "C" so the host library links them without templates).
 extern "C" {
 int mpcq_internal_setup_launch(const mpcq::SetupArgs *args, hipStream_t stream);
@@ -329,6 +345,9 @@ int mpcq_internal_set_step(long long *step, long long v, hipStream_t s);
 // (one 512-thread workgroup per QP: KKT inverse by Gauss-Jordan in VGPRs, structured A).
 int mpcq_internal_mimo_setup_launch(const mpcq::MimoSetupArgs *a, hipStream_t s);
 int mpcq_internal_mimo_solve_launch(const mpcq::MimoArgs *a, hipStream_t s);
+// One pass per batch of distinct SISO plants (mpcq_plant.hip): condensing + setup + one
+// controllerStep per plant, two plants per wave.  0 launched, -1 unsupported shape, -2 HIP error.
+int mpcq_internal_plant_step_launch(const mpcq::PlantStepArgs *a, int is_f32, hipStream_t s);
 // Build the TileLayout images (type T = f32 if is_f32) of plant 0 from its fp64 operator block.
 int mpcq_internal_tile_images(const double *ops, int nc, int mc, int KN, int KM, int is_f32, void *img,
                               hipStream_t s);

@@ -172,6 +172,21 @@ def flops_plant_setup(n: int, m: int, N: int | None = None) -> float:
     return (4 * N ** 3 + 10 * N ** 2 + 128 * N) + 30 * (n * n + n * m) + (2 * n * n * m + n ** 3 / 3 + n * n)
 
 
+def flops_plant_step(N: int, nx: int, iters, refactors, scaling: int = 10, check: int = 25) -> np.ndarray:
+    """FLOPs plant_step_kernel performs per plant (mpcq_plant.hip; FMA = 2, m = 2N with the paired rows):
+    condensing (the Ad^k Bd / Cd Ad^k recurrences 4 N nx^2, CAB 2 N nx, P rows ~N^3, Fu / Fr 1 / Fx
+    ~(6 + 2 nx) N^2 / 2), Ruiz (`scaling` passes over P and the N x N half of A: ~7 N^2 each), the KKT
+    matrix 4 N^3 and its Gauss-Jordan inverse 2 N^3 plus (A^ M^-1) 2 N^3 at setup and at every
+    refactorisation, the front end 2 N (nx + 2), and per iteration the three N x N products 6 N^2 plus
+    ~20 N element-wise, per check three more products 6 N^2 and ~30 N of norms."""
+    it = np.asarray(iters, dtype=np.float64)
+    cond = 4 * N * nx * nx + 2 * N * nx + N ** 3 + (6 + 2 * nx) * N * N / 2
+    ruiz = scaling * 7 * N * N
+    kkt = 8 * N ** 3
+    return (cond + ruiz + 2 * N * (nx + 2) + (1 + np.asarray(refactors, dtype=np.float64)) * kkt
+            + it * (6 * N * N + 20 * N) + np.floor(it / check) * (6 * N * N + 30 * N))
+
+
 # ----------------------------------------------------------------------------- config 4: quad-rotor
 QUAD = {  # hover linearisation of a small quad-rotor (BASELINE config 4: n_x 12, n_u 4, N 30, dt 0.02)
     "mass": 0.5, "inertia": (2.3e-3, 2.3e-3, 4.0e-3), "g": 9.81, "dt": 0.02, "spread": 0.10,

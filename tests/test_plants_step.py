@@ -1,0 +1,108 @@
+"""BASELINE config 3 in one pass (mpcq_mpc_plants_step_device, solvempc_amd/csrc/mpcq_plant.hip):
+every plant condensed, set up and stepped once with its operators kept on chip, against the oracle's
+reference constructor + controllerStep per plant (oracle/mpc_batch.c) on the same plants and states.
+
+Bar (every plant): fp64 — the oracle's status and iteration count, the applied U and the whole
+solution to 1e-9; fp32 — the oracle's status, its iteration count except on the oracle's own
+schedule ties (decision margin < TIE_MARGIN, see test_gpu.py), the applied move and the solution
+within 1e-5 * max(1, ||x||_inf).  Plus: agreement with the two-stage path (setup_plants + step), odd
+batch sizes (a half-empty last wave), other horizons, and the one-shot context contract."""
+import numpy as np
+import pytest
+
+import oracle
+import solvempc_amd as sm
+from solvempc_amd import workload
+
+pytestmark = pytest.mark.gpu
+TIE_MARGIN = 2e-3
+
+
+def _dev(a):
+    import torch
+
+    return torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64), device="cuda:0")
+
+
+def _plants(plant, B, seed):
+    Ad, Bd = workload.randomized_plants(plant, seed, 0, B)
+    X, U = workload.mpc_states(seed, 0, B)
+    return Ad, Bd, X, U
+
+
+def _plant_arrays(plant, Ad, Bd):
+    B = Ad.shape[0]
+    return [_dev(Ad), _dev(Bd), _dev(np.tile(plant["Cd"], (B, 1))), _dev(np.tile(plant["K"], (B, 1))),
+            _dev(np.full(B, plant["Q"])), _dev(np.full(B, plant["R"])), _dev(np.full(B, plant["RD"]))]
+
+
+def _fused(plant, Ad, Bd, X, U, N, dtype):
+    import torch
+
+    B = Ad.shape[0]
+    keep = _plant_arrays(plant, Ad, Bd)
+    Xd, Ud = _dev(X), _dev(U)
+    s = sm.BatchSolver(N, 2 * N, B, n_plants=B, dtype=dtype)
+    s.mpc_plants_step_device(4, 10, *[k.data_ptr() for k in keep], Xd.data_ptr(), Ud.data_ptr())
+    torch.cuda.synchronize()
+    return s, Ud.cpu().numpy()
+
+
+@pytest.mark.parametrize("N,B", [(20, 257), (15, 64), (32, 33)])
+def test_fp64_matches_oracle(plant, N, B):
+    Ad, Bd, X, U = _plants(plant, B, 2)
+    s, Ug = _fused(plant, Ad, Bd, X, U, N, "f64")
+    st, it, rho = s.info()
+    U_ref, st_ref, it_ref, x_ref, _ = oracle.plants_step(plant, Ad, Bd, X, U, N, full=True)
+    assert np.array_equal(st, st_ref) and np.all(st == sm.SOLVED)
+    assert np.array_equal(it, it_ref)
+    assert np.abs(Ug - U_ref).max() < 1e-9
+    assert np.abs(s.solution() - x_ref).max() < 1e-9
+
+
+def test_fp32_matches_oracle(plant):
+    N, B = 20, 2048
+    Ad, Bd, X, U = _plants(plant, B, 2)
+    s, Ug = _fused(plant, Ad, Bd, X, U, N, "f32")
+    st, it, _ = s.info()
+    U_ref, st_ref, it_ref, x_ref, margin = oracle.plants_step(plant, Ad, Bd, X, U, N, full=True)
+    assert np.array_equal(st, st_ref)
+    off = it != it_ref
+    assert not np.any(off & (margin >= TIE_MARGIN)), (np.flatnonzero(off)[:8], margin[off][:8])
+    scale = np.maximum(1.0, np.abs(x_ref).max(axis=1))
+    x = s.solution()
+    assert (np.abs(x - x_ref).max(axis=1)[~off] / scale[~off]).max() < 1e-5
+    assert (np.abs(Ug - U_ref)[~off] / scale[~off]).max() < 1e-5
+
+
+def test_agrees_with_two_stage_path(plant):
+    """The same plants through mpcq_mpc_setup_plants_device + mpcq_mpc_step_device (operators in HBM)."""
+    import torch
+
+    N, B = 20, 130
+    Ad, Bd, X, U = _plants(plant, B, 5)
+    sf, Uf = _fused(plant, Ad, Bd, X, U, N, "f64")
+    keep = _plant_arrays(plant, Ad, Bd)
+    Xd, Ud = _dev(X), _dev(U)
+    s2 = sm.BatchSolver(N, 2 * N, B, n_plants=B)
+    stream = torch.cuda.current_stream().cuda_stream
+    s2.mpc_setup_plants_device(4, 10, *[k.data_ptr() for k in keep], stream)
+    s2.mpc_step_device(Xd.data_ptr(), Ud.data_ptr(), 0.0, stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(sf.info()[0], s2.info()[0]) and np.array_equal(sf.info()[1], s2.info()[1])
+    assert np.abs(Uf - Ud.cpu().numpy()).max() < 1e-10
+    assert np.abs(sf.solution() - s2.solution()).max() < 1e-10
+    assert np.abs(sf.dual() - s2.dual()).max() < 1e-8
+
+
+def test_one_shot_context_contract(plant):
+    """After the one-pass step the context serves its results but no further solves until set up."""
+    from solvempc_amd import _capi
+
+    N, B = 20, 8
+    Ad, Bd, X, U = _plants(plant, B, 3)
+    s, _ = _fused(plant, Ad, Bd, X, U, N, "f64")
+    assert s.solution().shape == (B, N) and s.dual().shape == (B, 2 * N)
+    with pytest.raises(sm.MpcqError) as e:
+        s.solve()
+    assert e.value.code == _capi.MPCQ_ERR_ORDER
