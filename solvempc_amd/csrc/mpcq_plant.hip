@@ -69,47 +69,104 @@ __device__ inline double limit_scaling_p(double d)
     return d > kMaxScaling ? kMaxScaling : d;
 }
 
+// DPP move whose lanes without a source (row shifts) or outside the row mask RM read 0
+template <int CTRL, int RM = 0xF> __device__ __forceinline__ float dpp0(float v)
+{
+    return __uint_as_float((unsigned)__builtin_amdgcn_update_dpp(0, (int)__float_as_uint(v), CTRL, RM, 0xF, false));
+}
+template <int CTRL, int RM = 0xF> __device__ __forceinline__ double dpp0(double v)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, RM, 0xF, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, RM, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ float readlane_t(float v, int l)
+{
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ double readlane_t(double v, int l)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// Inclusive scans over the 32 lanes of each half (lane r = horizon step r), op with identity 0 (sums,
+// maxima of non-negative values).  Prefix: row_shr 1, 2, 4, 8 inside the 16-lane rows, then
+// row_bcast:15 into rows 1 and 3.  Suffix: row_shl 1, 2, 4, 8, then rows 0 and 2 take lane 16's /
+// lane 48's total.  Call with the whole wave active (DPP and readlane read other lanes).
+template <typename T, typename F> __device__ __forceinline__ T half_prefix(T v, F op)
+{
+    v = op(v, dpp0<0x111>(v));
+    v = op(v, dpp0<0x112>(v));
+    v = op(v, dpp0<0x114>(v));
+    v = op(v, dpp0<0x118>(v));
+    return op(v, dpp0<0x142, 0xA>(v));
+}
+template <typename T, typename F> __device__ __forceinline__ T half_suffix(T v, F op, int lane)
+{
+    v = op(v, dpp0<0x101>(v));
+    v = op(v, dpp0<0x102>(v));
+    v = op(v, dpp0<0x104>(v));
+    v = op(v, dpp0<0x108>(v));
+    const T s0 = readlane_t(v, 16), s1 = readlane_t(v, 48);
+    return (lane & 16) ? v : op(v, (lane & 32) ? s1 : s0);
+}
+template <typename T> __device__ __forceinline__ T psum(T v) { return half_prefix(v, [](T a, T b) { return a + b; }); }
+template <typename T> __device__ __forceinline__ T ssum(T v, int lane)
+{
+    return half_suffix(v, [](T a, T b) { return a + b; }, lane);
+}
+
 template <int NC> struct PlantLds {
     static constexpr int LD = NC + 1;  // odd row stride: column walks by lane are conflict-free
-    double Ph[NC * LD], Ah[NC * LD], Mi[NC * LD];
-    double CAB[NC], CS[NC], Dv[NC], Ev[NC], Dt[NC], Et[NC], qh[NC], sh[4];
+    double Ph[NC * LD];                // scaled P^ (row r by lane r); before that the condensing scratch
+    double CAB[NC], CS[NC], Dv[NC], Ev[NC], SE[NC], qh[NC], Ut[NC], Ub[NC], piv[NC], tmp[NC];
+    double sh[4];  // cost, 1 / cost, U, K0
 };
 
-// Gauss-Jordan inverse of this half's SPD matrix (n x n, stride LD) in place, lane r of the half
-// updating row r (its own row and the pivot row in registers; no pivoting: SPD).
+// Gauss-Jordan inverse of this half's SPD matrix (n x n; SPD: no pivoting), lane r holding row r in
+// registers.  Per pivot the owner publishes its row through LDS (one wave: the DS queue keeps the
+// order, wave_sync only pins the compiler's); every lane then updates its row in place.
 template <int NC>
-__device__ __forceinline__ bool gj_half(double *M, int n, int r)
+__device__ __forceinline__ bool gj_rows(double (&row)[NC], double *piv, int n, int r)
 {
-    constexpr int LD = NC + 1;
     bool ok = true;
-    for (int k = 0; k < n; k++) {
-        const double ip = 1.0 / M[k * LD + k];
-        if (!(M[k * LD + k] > 0.0)) ok = false;
-        double row[NC];
-        const double f = (r < n) ? M[r * LD + k] : 0.0;
 #pragma unroll
-        for (int j = 0; j < NC; j++) {
-            if (j >= n || r >= n) continue;
-            const double mk = M[k * LD + j];
-            double v;
-            if (r == k && j == k) v = ip;
-            else if (r == k) v = mk * ip;
-            else if (j == k) v = -f * ip;
-            else v = M[r * LD + j] - f * (mk * ip);
-            row[j] = v;
+    for (int k = 0; k < NC; k++) {
+        if (k >= n) continue;  // (uniform; continue keeps the loop fully unrollable)
+        if (r == k) {
+#pragma unroll
+            for (int j = 0; j < NC; j += 2) *(double2 *)(piv + j) = make_double2(row[j], row[j + 1]);
         }
-        __syncthreads();
+        wave_sync();
+        const double pk = piv[k];
+        const double ip = 1.0 / pk;
+        if (!(pk > 0.0)) ok = false;
+        const double f = row[k];
 #pragma unroll
-        for (int j = 0; j < NC; j++)
-            if (j < n && r < n) M[r * LD + j] = row[j];
-        __syncthreads();
+        for (int j = 0; j < NC; j += 2) {
+            const double2 m2 = *(const double2 *)(piv + j);
+            const double mk[2] = {m2.x, m2.y};
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const int jj = j + e;
+                double v;
+                if (r == k) v = (jj == k) ? ip : mk[e] * ip;
+                else v = (jj == k) ? -f * ip : row[jj] - f * (mk[e] * ip);
+                row[jj] = v;
+            }
+        }
+        wave_sync();
     }
     return ok;
 }
 
 template <typename T, int NC>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void plant_step_kernel(PlantStepArgs a)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 4))) void plant_step_kernel(PlantStepArgs a)
 {
+    static_assert(NC % 4 == 0, "broadcast rows are read 16 B at a time");
     constexpr int LD = NC + 1;
     __shared__ PlantLds<NC> lds[2];
     __shared__ __attribute__((aligned(16))) T bx[2][NC], bw[2][NC];  // per-half broadcasts
@@ -119,18 +176,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     const int p = live ? plant : 0;  // a dead half runs plant 0's data and publishes nothing
     const int N = a.N, n = N, nx = a.nx;
     const bool lr = r < N;
-    const int rr = lr ? r : 0;
     PlantLds<NC> &S = lds[h];
+    T *bxh = bx[h], *bwh = bw[h];
     const SolverSettings &st = a.st;
+    // cold-path views: lane indices re-derived opaquely, so the loop does not keep the addresses of
+    // the refactorisation, the checks and the finalize live in VGPRs across the hot iteration
+    auto cold_lane = [&]() { return opaque(lane); };
     if (r < NC) {  // broadcast slots beyond N stay zero (row_dot reads the whole capacity)
-        bx[h][r] = T(0);
-        bw[h][r] = T(0);
+        bxh[r] = T(0);
+        bwh[r] = T(0);
     }
 
     // ---------------------------------------------------------------- 1. condensing
     // CAB[k] = Cd Ad^k Bd and c_k = Cd Ad^k (Sx row k-1) by the recurrences v_{k+1} = Ad v_k,
-    // c_{k+1} = c_k Ad: lane t < nx of the half owns component t (scratch in Mi).
-    double *V = S.Mi, *Cr = S.Mi + (NC + 1) * 8;  // V[k][8], Cr[k][8] for k <= N
+    // c_{k+1} = c_k Ad: lane t < nx of the half owns component t (scratch in the P^ slot).
+    double *V = S.Ph, *Cr = S.Ph + (NC + 1) * 8;  // V[k][8], Cr[k][8] for k <= N
+    static_assert((NC + 1) * 16 <= NC * LD, "condensing scratch fits the P^ slot");
     {
         const double *Ad = a.Ad + (size_t)p * nx * nx, *Bd = a.Bd + (size_t)p * nx, *Cd = a.Cd + (size_t)p * nx;
         double adr[8], adc[8];  // row t and column t of Ad
@@ -143,7 +204,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
             V[r] = r < nx ? Bd[r] : 0.0;
             Cr[r] = r < nx ? Cd[r] : 0.0;
         }
-        __syncthreads();
+        wave_sync();
         for (int k = 0; k < N; k++) {
             double v = 0.0, c = 0.0;
 #pragma unroll
@@ -151,12 +212,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
                 v += adr[s] * V[k * 8 + s];
                 c += Cr[k * 8 + s] * adc[s];
             }
-            __syncthreads();
+            wave_sync();
             if (r < 8) {
                 V[(k + 1) * 8 + r] = v;
                 Cr[(k + 1) * 8 + r] = c;
             }
-            __syncthreads();
+            wave_sync();
         }
         if (lr) {
             double v = 0.0;
@@ -164,193 +225,203 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
             for (int s = 0; s < 8; s++) v += Cd[s < nx ? s : 0] * (s < nx ? V[r * 8 + s] : 0.0);
             S.CAB[r] = v;  // Cd Ad^r Bd
         }
-        __syncthreads();
+        wave_sync();
         if (r == 0) {
             double v = 0.0;
             for (int k = 0; k < N; k++) { v += S.CAB[k]; S.CS[k] = v; }  // Su(i, j) = CS[i - j]
         }
-        __syncthreads();
+        wave_sync();
     }
     const double Q = a.Q[p], R = a.R[p], RD = a.RD[p];
     const double *K = a.K + (size_t)p * nx;
     const double K0 = K[0];
-    // row r of P (setH :250-251: H1 = 2 (LL' Rbar LL + RbarD + Su' Qbar Su), symmetric as computed, so
-    // (H1 + H1') / 2 = H1), Fu[r] (:305, incl. the diagonal() quirk: R 1), Fr 1 xref (:306, :374),
-    // Fx row r (:307)
-    double Fu = 0.0, frr = 0.0, Fx[8];
-    if (lr) {
-        for (int j = 0; j < N; j++) {
-            const int mx = r > j ? r : j;
-            double t4 = 0.0;
-            for (int k = mx; k < N; k++) t4 += (S.CS[k - r] * Q) * S.CS[k - j];
-            S.Ph[r * LD + j] = 2.0 * ((R * (double)(N - mx) + (r == j ? RD : 0.0)) + t4);
-        }
-        double s1 = 0.0, sf = 0.0;
-        for (int k = r; k < N; k++) {
-            s1 += (S.CS[k] * Q) * S.CS[k - r];
-            sf += -2.0 * (Q * S.CS[k - r]) * a.xref;
-        }
-        Fu = 2.0 * (R + s1);
-        frr = sf;
-#pragma unroll
-        for (int c = 0; c < 8; c++) {
-            double v = 0.0;
-            if (c < nx)
-                for (int k = r; k < N; k++) v += (Cr[(k + 1) * 8 + c] * Q) * S.CS[k - r];
-            Fx[c] = 2.0 * v;
-        }
-        for (int j = 0; j < N; j++) S.Ah[r * LD + j] = (j <= r) ? K0 : 0.0;  // top half of Gbar
-        S.Dv[r] = 1.0;
-        S.Ev[r] = 1.0;
-        S.qh[r] = 0.0;  // the ctor's setup gradient (X = U = 0, xref = 0 in the reference config)
-    }
-    if (r == 0) S.sh[0] = 1.0;
-    __syncthreads();
-
-    // ---------------------------------------------------------------- 2. scale_data (Ruiz)
-    // setup_inv_kernel's arithmetic; the bottom rows of A are the negated top rows, so their column
-    // and row norms are the top ones and E is the same for rows r and N + r.
-    double cp = 1.0;
-    for (int it = 0; it < st.scaling; it++) {
-        if (lr) {
-            double vp = 0.0, va = 0.0, ve = 0.0;
-            for (int i = 0; i < n; i++) vp = fmax(vp, fabs(S.Ph[i * LD + r]));
-            for (int i = 0; i < n; i++) va = fmax(va, fabs(S.Ah[i * LD + r]));
-            for (int j = 0; j < n; j++) ve = fmax(ve, fabs(S.Ah[r * LD + j]));
-            S.Dt[r] = 1.0 / sqrt(limit_scaling_p(fmax(cp * vp, va)));
-            S.Et[r] = 1.0 / sqrt(limit_scaling_p(ve));
-        }
-        __syncthreads();
-        if (lr) {
-            const double dr = S.Dt[r], er = S.Et[r];
-            for (int k = 0; k < n; k++) {
-                S.Ph[r * LD + k] = (dr * (S.Ph[r * LD + k] * cp)) * S.Dt[k];
-                S.Ah[r * LD + k] = (er * S.Ah[r * LD + k]) * S.Dt[k];
-            }
-            S.qh[r] *= dr;
-            S.Dv[r] *= dr;
-            S.Ev[r] *= er;
-        }
-        __syncthreads();
-        if (lr) {
-            double v = 0.0;
-            for (int i = 0; i < n; i++) v = fmax(v, fabs(S.Ph[i * LD + r]));
-            S.Dt[r] = v;
-        }
-        __syncthreads();
-        if (r == 0) {
-            double mean = 0.0, qn = 0.0;
-            for (int j = 0; j < n; j++) mean += S.Dt[j];
-            mean /= n;
-            for (int j = 0; j < n; j++) qn = fmax(qn, fabs(S.qh[j]));
-            qn = limit_scaling_p(qn);
-            const double ct = 1.0 / limit_scaling_p(fmax(mean, qn));
-            S.sh[1] = ct;
-            S.sh[0] *= ct;
-        }
-        __syncthreads();
-        cp = S.sh[1];
-        if (lr) S.qh[r] *= cp;
-    }
-    if (st.scaling > 0) {
-        if (lr)
-            for (int k = 0; k < n; k++) S.Ph[r * LD + k] *= cp;
-        __syncthreads();
-    }
-    const double cost = S.sh[0], cinv = 1.0 / cost;
-    // set_rho_vec: l = -DBL_MAX (:42) and u0 = W0 = 255 (:43, X = U = 0): every row an inequality
-    // (the rows' type is checked again below against this step's bounds)
-    const double Er = lr ? S.Ev[r] : 1.0, Dr = lr ? S.Dv[r] : 1.0;
-
-    // ---------------------------------------------------------------- 3. M(rho)^-1, operator rows
-    T Srow[NC], Btc[NC], Brow[NC];  // sigma M^-1 row r; (A^ M^-1) column r (top rows); A^ row r
-    auto build_inverse = [&](double rho) -> bool {
-        __syncthreads();
-        if (lr)
-            for (int k = 0; k < n; k++) {
-                double v = S.Ph[r * LD + k] + (r == k ? st.sigma : 0.0);
-                for (int pass = 0; pass < 2; pass++)  // rows j (top) then N + j (bottom: (-a)(-a)' = a a')
-                    for (int j = 0; j < n; j++) v += rho * (S.Ah[j * LD + r] * S.Ah[j * LD + k]);
-                S.Mi[r * LD + k] = v;
-            }
-        __syncthreads();
-        const bool ok = gj_half<NC>(S.Mi, n, r);
-#pragma unroll
-        for (int i = 0; i < NC; i++) {
-            Srow[i] = (lr && i < n) ? (T)(st.sigma * S.Mi[rr * LD + i]) : T(0);
-            Brow[i] = (lr && i < n) ? (T)S.Ah[rr * LD + i] : T(0);
-            double bt = 0.0;
-            if (lr && i < n)
-                for (int k = 0; k < n; k++) bt += S.Ah[i * LD + k] * S.Mi[k * LD + rr];
-            Btc[i] = (T)bt;
-        }
-        return ok;
-    };
-    const double rho0 = fmin(fmax(st.rho, kRhoMin), kRhoMax);
-    const bool setup_ok = build_inverse(rho0);
-
-    // ---------------------------------------------------------------- 4. controllerStep
+    // this step's inputs (controllerStep: X, U), read now so the condensing's Fx row is consumed here
     double Xv[8];
     const double *Xp = a.X + (size_t)p * nx;
 #pragma unroll
     for (int c = 0; c < 8; c++) Xv[c] = c < nx ? Xp[c] : 0.0;
     const double Uv = a.U[p];
+    // row r of P (setH :250-251: H1 = 2 (LL' Rbar LL + RbarD + Su' Qbar Su), symmetric as computed, so
+    // (H1 + H1') / 2 = H1), in registers; Fu[r] (:305, incl. the diagonal() quirk: R 1), Fr 1 xref
+    // (:306, :374) and Fx row r (:307) fold straight into q = Fx X + Fu U + Fr ref (setF, :374)
+    double pr[NC];
+#pragma unroll
+    for (int j = 0; j < NC; j++) {
+        double v = 0.0;
+        if (lr && j < N) {
+            const int mx = r > j ? r : j;
+            double t4 = 0.0;
+            for (int k = mx; k < N; k++) t4 += (S.CS[k - r] * Q) * S.CS[k - j];
+            v = 2.0 * ((R * (double)(N - mx) + (r == j ? RD : 0.0)) + t4);
+        }
+        pr[j] = v;
+    }
+    double qk = 0.0;
+    if (lr) {
+        double s1 = 0.0, sf = 0.0;
+        for (int k = r; k < N; k++) {
+            s1 += (S.CS[k] * Q) * S.CS[k - r];
+            sf += -2.0 * (Q * S.CS[k - r]) * a.xref;
+        }
+        const double Fu = 2.0 * (R + s1);
+        double s0 = 0.0;
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+            double v = 0.0;
+            if (c < nx)
+                for (int k = r; k < N; k++) v += (Cr[(k + 1) * 8 + c] * Q) * S.CS[k - r];
+            if (c < nx) s0 += (2.0 * v) * Xv[c];
+        }
+        qk = s0 + Fu * Uv + sf;
+    }
     double kx = 0.0;  // K X (Sbar rows < s_rows, :185,208)
 #pragma unroll
     for (int c = 0; c < 8; c++)
         if (c < nx) kx += K[c] * Xv[c];
-    T qh = T(0), ut = T(kInfty), ub = T(kInfty);
-    double qs = 0.0;
-    if (lr) {
-        double s0 = 0.0;
+
+    // ---------------------------------------------------------------- 2. scale_data (Ruiz)
+    // setup_inv_kernel's arithmetic with A structural: the top half of Gbar is K0 L (L lower-triangular
+    // ones, :332-347) and the bottom half its negation, so A^ = E K0 L D entrywise, its column norms are
+    // |K0| D_r max_{i >= r} E_i (suffix maxima) and its row norms |K0| E_r max_{k <= r} D_k (prefix
+    // maxima); P is symmetric, so its column norm is lane r's row maximum.  The ctor's gradient is zero
+    // (X = U = 0, xref = 0), so the cost scaling's |q| term is limit_scaling(0) = 1.
+    const double aK0 = fabs(K0);
+    double Dr = lr ? 1.0 : 0.0, Er = lr ? 1.0 : 0.0;  // (0 on dead lanes: neutral in every scan)
+    double cost = 1.0, cp = 1.0;
+    auto dmax = [](double x, double y) { return fmax(x, y); };
+    for (int it = 0; it < st.scaling; it++) {
+        double vp = 0.0;
 #pragma unroll
-        for (int c = 0; c < 8; c++)
-            if (c < nx) s0 += Fx[c] * Xv[c];
-        const double qk = s0 + Fu * Uv + frr;                 // setF (:374)
+        for (int j = 0; j < NC; j++) vp = fmax(vp, fabs(pr[j]));
+        const double emax = half_suffix(Er, dmax, lane), dpre = half_prefix(Dr, dmax);
+        const double va = (aK0 * Dr) * emax, ve = (aK0 * Er) * dpre;
+        const double dt = 1.0 / sqrt(limit_scaling_p(fmax(cp * vp, va)));
+        const double et = 1.0 / sqrt(limit_scaling_p(ve));
+        if (r < NC) S.tmp[r] = lr ? dt : 0.0;
+        wave_sync();
+        double cn = 0.0;
+#pragma unroll
+        for (int j = 0; j < NC; j += 2) {
+            const double2 d2 = *(const double2 *)(S.tmp + j);
+            pr[j] = (dt * (pr[j] * cp)) * d2.x;
+            pr[j + 1] = (dt * (pr[j + 1] * cp)) * d2.y;
+            cn = fmax(cn, fmax(fabs(pr[j]), fabs(pr[j + 1])));
+        }
+        wave_sync();
+        if (lr) { Dr *= dt; Er *= et; }
+        const double mean = hsum(lr ? cn : 0.0) / n;
+        cp = 1.0 / limit_scaling_p(fmax(mean, 1.0));
+        cost *= cp;
+    }
+    if (st.scaling > 0) {
+#pragma unroll
+        for (int j = 0; j < NC; j++) pr[j] *= cp;
+    }
+    const double cinv = 1.0 / cost;
+    if (r < NC) {
+#pragma unroll
+        for (int j = 0; j < NC; j++) S.Ph[r * LD + j] = pr[j];  // (zero rows beyond N)
+        S.Dv[r] = Dr;
+        S.Ev[r] = Er;
+    }
+    {
+        const double se = ssum(Er * Er, lane);  // sum_{i >= r} E_i^2: A^'A^ = 2 K0^2 D_r D_k SE[max(r, k)]
+        if (r < NC) S.SE[r] = se;
+    }
+
+    // ---------------------------------------------------------------- 3. controllerStep front end
+    T qh = T(0), ut = T(kInfty), ub = T(kInfty);
+    double qs = 0.0, up_t = 0.0, up_b = 0.0;
+    if (lr) {
         const double sx = r < a.s_rows ? kx : 0.0;
-        const double up_t = 255.0 + sx + (-K0) * Uv;          // W0 + Sbar X + Ku U (:43, :99)
-        const double up_b = 255.0 + (-sx) + K0 * Uv;
+        up_t = 255.0 + sx + (-K0) * Uv;                      // W0 + Sbar X + Ku U (:43, :99)
+        up_b = 255.0 + (-sx) + K0 * Uv;
         qs = (qk * Dr) * cost;                                // q^ = c D q (osqp_update_lin_cost)
         qh = (T)qs;
         ut = (T)(up_t * Er);                                  // u^ = E u (osqp_update_upper_bound)
         ub = (T)(up_b * Er);
     }
+    if (r < NC) {  // the values only the checks and the finalize read stay in LDS (read there, after
+                   // the loop's wave_syncs: not hoisted into registers for the whole solve)
+        S.qh[r] = (double)qh;  // q^ as the iteration sees it
+        S.Ut[r] = up_t;
+        S.Ub[r] = up_b;
+    }
+    if (r == 0) {
+        S.sh[0] = cost;
+        S.sh[1] = cinv;
+        S.sh[2] = Uv;
+        S.sh[3] = K0;
+    }
     // the update's checks (l^ = -DBL_MAX E stays free of -OSQP_INFTY MIN_SCALING): u < l cannot occur;
     // a row whose u^ reaches OSQP_INFTY MIN_SCALING would change type (TYPE_CHANGED)
     int status = hany(lr && ((double)ut > kInfty * kMinScaling || (double)ub > kInfty * kMinScaling)) ? kTypeChanged
                                                                                                      : kUnsolved;
-    if (!setup_ok) status = kNonCvx;
-    if (!live) status = kSolved;  // (never published)
-    // g = -M^-1 q^ (column r of the symmetric M^-1)
-    auto make_g = [&]() -> T {
-        double g = 0.0;
-        if (lr)
-            for (int i = 0; i < n; i++) g += S.Mi[i * LD + r] * (double)(T)S.qh[i];
-        return lr ? (T)(-g) : T(0);
-    };
-    __syncthreads();
-    if (lr) S.qh[r] = qs;  // (the setup copy of q^ is dead: reuse its slot for this step's q^)
-    __syncthreads();
-    T gk = make_g();
 
+    // ---------------------------------------------------------------- 4. ADMM
+    // M(rho) = P^ + sigma I + rho A^'A^ (set_rho_vec: every row an inequality at rho) and its inverse
+    // row r; in registers sigma M^-1 row r (Srow) and column r of (A^ M^-1)' (Btc: A^ M^-1 = E K0 L D M^-1,
+    // so Btc[i] = E_i K0 sum_{k<=i} D_k M^-1_kr, a prefix over this lane's own row), g = -M^-1 q^.
+    // An iteration: x~ = g + Srow x + Btc (w_top - w_bot) (one broadcast round: the (A^ M^-1) product
+    // formed in fp64 keeps the fp32 iterate as accurate as the dense operators), z~ = A^ x~ (a prefix
+    // scan).
+    T Srow[NC], Btc[NC];
+    T gk = T(0);
+    const double Dd = lr ? Dr : 0.0, A2 = 2.0 * K0 * K0;
+    auto factor = [&](double rho) -> bool {
+        const int cl = cold_lane(), r = cl & 31;
+        PlantLds<NC> &S = lds[cl >> 5];
+        double row[NC];
+#pragma unroll
+        for (int j = 0; j < NC; j++) {
+            double v = 0.0;
+            if (lr && j < n) {
+                const int mx = r > j ? r : j;
+                v = S.Ph[r * LD + j] + (r == j ? st.sigma : 0.0) + rho * (((A2 * Dd) * S.Dv[j]) * S.SE[mx]);
+            }
+            row[j] = v;
+        }
+        const bool ok = gj_rows<NC>(row, S.piv, n, r);
+        double g = 0.0, pre = 0.0;
+#pragma unroll
+        for (int j = 0; j < NC; j += 2) {
+            const double2 q2 = *(const double2 *)(S.qh + j);
+            const double2 d2 = *(const double2 *)(S.Dv + j);
+            const double2 e2 = *(const double2 *)(S.Ev + j);
+            g = fma(row[j], q2.x, g);
+            g = fma(row[j + 1], q2.y, g);
+            Srow[j] = (T)(st.sigma * row[j]);
+            Srow[j + 1] = (T)(st.sigma * row[j + 1]);
+            pre += d2.x * row[j];
+            Btc[j] = (T)((e2.x * K0) * pre);
+            pre += d2.y * row[j + 1];
+            Btc[j + 1] = (T)((e2.y * K0) * pre);
+        }
+        gk = lr ? (T)(-g) : T(0);
+        return ok;
+    };
+
+    const double rho0 = fmin(fmax(st.rho, kRhoMin), kRhoMax);
     T xs = T(0), zt = T(0), zb = T(0), yt = T(0), yb = T(0);
     T rho = (T)rho0, rinv = T(1) / rho;
     const T alpha = (T)st.alpha, oma = T(1) - (T)st.alpha;
-    const T eps_abs = (T)st.eps_abs, eps_rel = (T)st.eps_rel;
-    const T EiT = (T)(1.0 / Er), DiT = (T)(1.0 / Dr), ErT = (T)Er, cinvT = (T)cinv;
+    const T ET = (T)(lr ? Er : 0.0), DT = (T)Dd, K0T = (T)K0;
+    const T EK = ET * K0T;  // (A^ x)_r = E_r K0 sum_{k<=r} D_k x_k
     const bool scaled_term = st.scaled_termination != 0;
     const int ct = st.check_termination;
     const int ai = (st.adaptive_rho && a.adaptive_interval) ? a.adaptive_interval : 0;
     int next_check = ct ? ct : -1, next_adapt = ai ? ai : -1;
     int it = 0;
-    bool done = status != kUnsolved;
-    bool refactor = false;
-    T *bxh = bx[h], *bwh = bw[h];
+    bool done = false, setup_ok = true, first = true, refactor = true;
 
     auto finalize = [&]() {
+        const int cl = cold_lane(), r = cl & 31;
+        const PlantLds<NC> &S = lds[cl >> 5];
+        const int plant = blockIdx.x * 2 + (cl >> 5);
         const bool has_sol = status == kSolved || status == kSolvedInaccurate || status == kMaxIterReached;
         if (!live) return;
         if (lr) {
+            const double Er = S.Ev[r], Dr = S.Dv[r], cinv = S.sh[1], Uv = S.sh[2];
             const double xv = has_sol ? (double)xs * Dr : __builtin_nan("");
             a.x[(size_t)plant * n + r] = xv;
             if (r == 0) {
@@ -363,15 +434,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
             a.y[(size_t)plant * 2 * n + n + r] = has_sol ? ((double)yb * Er) * cinv : __builtin_nan("");
         }
     };
-    if (done) finalize();
+    // P^ v for this half (row r of P^ from LDS, v broadcast)
+    auto p_times = [&](T v) -> double {
+        const int cl = cold_lane(), r = cl & 31;
+        PlantLds<NC> &S = lds[cl >> 5];
+        T *bxh = bx[cl >> 5];
+        if (r < NC) bxh[r] = lr ? v : T(0);
+        wave_sync();
+        double acc = 0.0;
+        if (lr)
+            for (int i = 0; i < n; i++) acc = fma(S.Ph[r * LD + i], (double)bxh[i], acc);
+        wave_sync();
+        return acc;
+    };
 
-    while (!wave_all(done)) {
-        if (refactor) {  // OSQP's KKT refactorisation after a rho change (each half at its own rho; a
-                         // half whose rho did not move rebuilds the same bits)
-            build_inverse((double)rho);
-            gk = make_g();
+    for (;;) {
+        if (refactor) {  // initSolver's factorisation, then OSQP's refactorisation after a rho change (each
+                         // half at its own rho; a half whose rho did not move rebuilds the same bits)
+            const bool ok = factor(first ? rho0 : (double)rho);
             refactor = false;
+            if (first) {
+                first = false;
+                setup_ok = ok;
+                if (!ok) status = kNonCvx;
+                if (!live) status = kSolved;  // (never published)
+                done = status != kUnsolved;
+                if (done) finalize();
+            }
         }
+        if (wave_all(done)) break;
         it++;
         const bool at_check = it == next_check, at_adapt = it == next_adapt;
         if (at_check) next_check += ct;
@@ -379,20 +470,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
         const bool last = it == st.max_iter;
         const bool info = at_check || at_adapt || last;
 
-        // xi = g + sigma M^-1 x + (A^ M^-1)' (w_top - w_bot),  w = rho z - y
+        // x~ = g + sigma M^-1 x + (A^ M^-1)' (w_top - w_bot),  w = rho z - y
         const T wt = tt_fma(rho, zt, -yt) - tt_fma(rho, zb, -yb);
-        __syncthreads();
-        if (lr) { bxh[r] = xs; bwh[r] = wt; }
-        __syncthreads();
+        if (r < NC) {
+            bxh[r] = lr ? xs : T(0);
+            bwh[r] = lr ? wt : T(0);
+        }
+        wave_sync();
         const T xi = row_dot(Srow, bxh, gk) + row_dot(Btc, bwh, T(0));
+        wave_sync();
         const T xn = lr ? tt_fma(alpha, xi, oma * xs) : T(0);
         const T dx = xn - xs;
         if (!done) xs = xn;
         // z~ = A^ x~ (top rows; bottom = -top), relaxation, projection onto [l, u], dual update
-        __syncthreads();
-        if (lr) bxh[r] = xi;
-        __syncthreads();
-        const T zz = row_dot(Brow, bxh, T(0));
+        const T zz = EK * psum(DT * xi);
         T dyt = T(0), dyb = T(0);
         if (lr && !done) {
             T v = tt_fma(alpha, zz, oma * zt);
@@ -408,90 +499,91 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
         }
         if (!info) continue;
 
-        // ---- update_info: residuals (half-wave reductions)
-        __syncthreads();
-        if (lr) { bxh[r] = xs; bwh[r] = yt - yb; }
-        __syncthreads();
-        T ax_z = 0, ax_zs = 0, zn_s = 0, zn_r = 0, axn_s = 0, axn_r = 0;
-        T dr_r = 0, dr_s = 0, qn_r = 0, qn_s = 0, atyn_r = 0, atyn_s = 0, pxn_r = 0, pxn_s = 0;
+        // ---- update_info: residuals, norms, certificates and the rho estimate in fp64 from the T
+        // iterate (exact in fp64), so an fp32 kernel takes OSQP's decisions on the same numbers as an
+        // fp64 one does on its own iterate (half-wave reductions)
+        using TD = double;
+        const int cl = cold_lane(), rc = cl & 31;
+        const PlantLds<NC> &C = lds[cl >> 5];
+        const TD Erl = lr ? C.Ev[rc] : 1.0, Drl = lr ? C.Dv[rc] : 1.0, Ddl = lr ? Drl : 0.0, qsl = lr ? C.qh[rc] : 0.0;
+        const TD utl = lr ? C.Ut[rc] : 0.0, ubl = lr ? C.Ub[rc] : 0.0;
+        const TD costl = C.sh[0], cinvl = C.sh[1], K0l = C.sh[3];
+        const TD xd = (TD)xs, ztd = (TD)zt, zbd = (TD)zb, ytd = (TD)yt, ybd = (TD)yb, dxd = (TD)dx;
+        const TD EKd = lr ? Erl * K0l : 0.0, DKd = Ddl * K0l, Ed = lr ? Erl : 0.0;
+        const TD EiD = 1.0 / Erl, DiD = 1.0 / Drl;
+        const TD utd = lr ? utl * Erl : 0.0, ubd = lr ? ubl * Erl : 0.0;  // (== (T) bounds for fp64)
+        const TD ax = EKd * psum(Ddl * xd);
+        const TD aty = DKd * ssum(Ed * (ytd - ybd), lane);
+        const TD px = p_times(xs);
+        TD ax_z = 0, ax_zs = 0, zn_s = 0, zn_r = 0, axn_s = 0, axn_r = 0;
+        TD dr_r = 0, dr_s = 0, qn_r = 0, qn_s = 0, atyn_r = 0, atyn_s = 0, pxn_r = 0, pxn_s = 0;
         if (lr) {
-            const T ax = row_dot(Brow, bxh, T(0));
-            const T r1 = ax - zt, r2 = -ax - zb;
-            ax_z = __builtin_fmax(__builtin_fabs(r1), __builtin_fabs(r2));
-            ax_zs = __builtin_fmax(__builtin_fabs(EiT * r1), __builtin_fabs(EiT * r2));
-            zn_r = __builtin_fmax(__builtin_fabs(zt), __builtin_fabs(zb));
-            zn_s = __builtin_fmax(__builtin_fabs(EiT * zt), __builtin_fabs(EiT * zb));
-            axn_r = __builtin_fabs(ax);
-            axn_s = __builtin_fabs(EiT * ax);
-            T px = T(0), aty = T(0);
-            for (int i = 0; i < n; i++) {
-                px = tt_fma((T)S.Ph[r * LD + i], bxh[i], px);
-                aty = tt_fma((T)S.Ah[i * LD + r], bwh[i], aty);
-            }
-            const T rd = (qh + px) + aty;
-            dr_r = __builtin_fabs(rd);
-            dr_s = __builtin_fabs(DiT * rd);
-            qn_r = __builtin_fabs(qh);
-            qn_s = __builtin_fabs(DiT * qh);
-            atyn_r = __builtin_fabs(aty);
-            atyn_s = __builtin_fabs(DiT * aty);
-            pxn_r = __builtin_fabs(px);
-            pxn_s = __builtin_fabs(DiT * px);
+            const TD r1 = ax - ztd, r2 = -ax - zbd;
+            ax_z = fmax(fabs(r1), fabs(r2));
+            ax_zs = fmax(fabs(EiD * r1), fabs(EiD * r2));
+            zn_r = fmax(fabs(ztd), fabs(zbd));
+            zn_s = fmax(fabs(EiD * ztd), fabs(EiD * zbd));
+            axn_r = fabs(ax);
+            axn_s = fabs(EiD * ax);
+            const TD rd = (qsl + px) + aty;
+            dr_r = fabs(rd);
+            dr_s = fabs(DiD * rd);
+            qn_r = fabs(qsl);
+            qn_s = fabs(DiD * qsl);
+            atyn_r = fabs(aty);
+            atyn_s = fabs(DiD * aty);
+            pxn_r = fabs(px);
+            pxn_s = fabs(DiD * px);
         }
         ax_z = hmax(ax_z); ax_zs = hmax(ax_zs); zn_s = hmax(zn_s); zn_r = hmax(zn_r);
         axn_s = hmax(axn_s); axn_r = hmax(axn_r);
         dr_r = hmax(dr_r); dr_s = hmax(dr_s); qn_r = hmax(qn_r); qn_s = hmax(qn_s);
         atyn_r = hmax(atyn_r); atyn_s = hmax(atyn_s); pxn_r = hmax(pxn_r); pxn_s = hmax(pxn_s);
-        const T pri_res = scaled_term ? ax_z : ax_zs;
-        const T dua_res = scaled_term ? dr_r : cinvT * dr_s;
+        const TD pri_res = scaled_term ? ax_z : ax_zs;
+        const TD dua_res = scaled_term ? dr_r : cinvl * dr_s;
 
-        // OSQP is_primal_infeasible on delta_y (l = -inf: d = max(dy, 0) on every row)
-        auto primal_infeasible = [&](T eps) -> bool {
-            const T d1 = tt_max(dyt, T(0)), d2 = tt_max(dyb, T(0));
-            T ndy = lr ? __builtin_fmax(__builtin_fabs(scaled_term ? d1 : ErT * d1), __builtin_fabs(scaled_term ? d2 : ErT * d2)) : T(0);
-            T lhs = lr ? ut * d1 + ub * d2 : T(0);
+        // OSQP is_primal_infeasible on delta_y (l = -inf: d = max(dy, 0) on every row); the A^'d product
+        // only when some half is a candidate
+        auto primal_infeasible = [&](TD eps) -> bool {
+            const TD d1 = fmax((TD)dyt, 0.0), d2 = fmax((TD)dyb, 0.0);
+            TD ndy = lr ? fmax(fabs(scaled_term ? d1 : Erl * d1), fabs(scaled_term ? d2 : Erl * d2)) : 0.0;
+            TD lhs = lr ? utd * d1 + ubd * d2 : 0.0;
             ndy = hmax(ndy);
             lhs = hsum(lhs);
-            const bool cand = ndy > T(kDivisionTol) && lhs < eps * ndy;
-            __syncthreads();
-            if (lr) bwh[r] = d1 - d2;
-            __syncthreads();
-            T atd = T(0);
-            if (lr)
-                for (int i = 0; i < n; i++) atd = tt_fma((T)S.Ah[i * LD + r], bwh[i], atd);
-            const T nat = hmax(lr ? __builtin_fabs(scaled_term ? atd : DiT * atd) : T(0));
+            const bool cand = ndy > kDivisionTol && lhs < eps * ndy;
+            if (!wave_any(cand)) return false;
+            const TD atd = DKd * ssum(Ed * (d1 - d2), lane);
+            const TD nat = hmax(lr ? fabs(scaled_term ? atd : DiD * atd) : 0.0);
             return cand && nat < eps * ndy;
         };
-        // OSQP is_dual_infeasible on delta_x
-        auto dual_infeasible = [&](T eps) -> bool {
-            const T qdx = hsum(lr ? qh * dx : T(0));
-            __syncthreads();
-            if (lr) bxh[r] = dx;
-            __syncthreads();
-            T t2 = T(0);
-            if (lr)
-                for (int i = 0; i < n; i++) t2 = tt_fma((T)S.Ph[r * LD + i], bxh[i], t2);
-            const T t3 = row_dot(Brow, bxh, T(0));
-            const T ndx = hmax(lr ? __builtin_fabs(scaled_term ? dx : (T)Dr * dx) : T(0));
-            const T cs = scaled_term ? T(1) : (T)cost;
-            const T npdx = hmax(lr ? __builtin_fabs(scaled_term ? t2 : DiT * t2) : T(0));
-            const T sv = scaled_term ? t3 : EiT * t3;
+        // OSQP is_dual_infeasible on delta_x; the P^ dx and A^ dx products only when some half is a
+        // candidate
+        auto dual_infeasible = [&](TD eps) -> bool {
+            const TD qdx = hsum(lr ? qsl * dxd : 0.0);
+            const TD ndx = hmax(lr ? fabs(scaled_term ? dxd : Drl * dxd) : 0.0);
+            const TD cs = scaled_term ? 1.0 : costl;
+            const bool cand = ndx > kDivisionTol && qdx < -cs * eps * ndx;
+            if (!wave_any(cand)) return false;
+            const TD t2 = p_times(dx);
+            const TD t3 = EKd * psum(Ddl * dxd);
+            const TD npdx = hmax(lr ? fabs(scaled_term ? t2 : DiD * t2) : 0.0);
+            const TD sv = scaled_term ? t3 : EiD * t3;
             const bool viol = hany(lr && (sv > eps * ndx || -sv > eps * ndx));  // rows r (u finite), N + r (-A x)
-            return ndx > T(kDivisionTol) && qdx < -cs * eps * ndx && npdx < cs * eps * ndx && !viol;
+            return cand && npdx < cs * eps * ndx && !viol;
         };
         auto check_termination = [&](bool approx) -> int {
-            const T mul = approx ? T(10) : T(1);
-            if (pri_res > T(kInfty) || dua_res > T(kInfty)) return kNonCvx;
-            const T ea = eps_abs * mul, er = eps_rel * mul;
+            const TD mul = approx ? 10.0 : 1.0;
+            if (pri_res > kInfty || dua_res > kInfty) return kNonCvx;
+            const TD ea = st.eps_abs * mul, er = st.eps_rel * mul;
             bool prim_ok = false, dual_ok = false, prim_inf = false, dual_inf = false;
-            const T ep = ea + er * (scaled_term ? tt_max(zn_r, axn_r) : tt_max(zn_s, axn_s));
+            const TD ep = ea + er * (scaled_term ? fmax(zn_r, axn_r) : fmax(zn_s, axn_s));
             if (pri_res < ep) prim_ok = true;
-            const bool pi = primal_infeasible((T)st.eps_prim_inf * mul);  // (uniform: evaluated for both halves)
+            const bool pi = primal_infeasible(st.eps_prim_inf * mul);  // (uniform: evaluated for both halves)
             if (!prim_ok) prim_inf = pi;
-            const T ed = ea + er * (scaled_term ? tt_max(tt_max(qn_r, atyn_r), pxn_r)
-                                                : cinvT * tt_max(tt_max(qn_s, atyn_s), pxn_s));
+            const TD ed = ea + er * (scaled_term ? fmax(fmax(qn_r, atyn_r), pxn_r)
+                                                 : cinvl * fmax(fmax(qn_s, atyn_s), pxn_s));
             if (dua_res < ed) dual_ok = true;
-            const bool di = dual_infeasible((T)st.eps_dual_inf * mul);
+            const bool di = dual_infeasible(st.eps_dual_inf * mul);
             if (!dual_ok) dual_inf = di;
             if (prim_ok && dual_ok) return approx ? kSolvedInaccurate : kSolved;
             if (prim_inf) return approx ? kPrimalInfeasibleInaccurate : kPrimalInfeasible;
@@ -505,13 +597,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
             if (!done && s0 != kUnsolved) { status = s0; term = true; }
         }
         if (!term && at_adapt) {
-            const T pr = ax_z / (tt_max(zn_r, axn_r) + T(kDivisionTol));
-            const T dn = tt_max(tt_max(qn_r, atyn_r), pxn_r);
-            const T du = dr_r / (dn + T(kDivisionTol));
-            T rn = rho * (T)sqrt((double)(pr / (du + T(kDivisionTol))));
-            rn = tt_min(tt_max(rn, T(kRhoMin)), T(kRhoMax));
-            if (!done && (rn > rho * (T)st.adaptive_rho_tolerance || rn < rho / (T)st.adaptive_rho_tolerance)) {
-                rho = tt_min(tt_max(rn, T(kRhoMin)), T(kRhoMax));
+            const TD rhod = (TD)rho;
+            const TD pr_ = ax_z / (fmax(zn_r, axn_r) + kDivisionTol);
+            const TD dn = fmax(fmax(qn_r, atyn_r), pxn_r);
+            const TD du = dr_r / (dn + kDivisionTol);
+            TD rn = rhod * sqrt(pr_ / (du + kDivisionTol));
+            rn = fmin(fmax(rn, kRhoMin), kRhoMax);
+            if (!done && (rn > rhod * st.adaptive_rho_tolerance || rn < rhod / st.adaptive_rho_tolerance)) {
+                rho = (T)rn;
                 rinv = T(1) / rho;
                 refactor = true;
             }
