@@ -12,6 +12,7 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 rc=$?; echo "smoke rc=$rc" >> gpurun_out/smoke.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 for wl in ${BENCH_WORKLOADS:-cfg2}; do
+  [ "$wl" = none ] && continue
   timeout -k 10 300 python bench.py --workload $wl --steps ${BENCH_STEPS:-10} --warmup 2 --cpu-seconds ${CPU_SECONDS:-4} > gpurun_out/bench_$wl.json 2> gpurun_out/bench_$wl.err
   rc=$?; if [ $rc -ne 0 ]; then echo "bench $wl rc=$rc" >> gpurun_out/bench_$wl.err; exit $rc; fi
 done

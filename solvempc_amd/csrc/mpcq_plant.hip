@@ -51,7 +51,7 @@ template <typename T, typename F> __device__ __forceinline__ T half_reduce(T v, 
 }
 template <typename T> __device__ __forceinline__ T hmax(T v)
 {
-    return half_reduce(v, [](T a, T b) { return __builtin_fmax(a, b); });
+    return half_reduce(v, [](T a, T b) { return tt_fmax(a, b); });
 }
 template <typename T> __device__ __forceinline__ T hsum(T v)
 {
@@ -164,7 +164,10 @@ __device__ __forceinline__ bool gj_rows(double (&row)[NC], double *piv, int n, i
 }
 
 template <typename T, int NC>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 4))) void plant_step_kernel(PlantStepArgs a)
+#ifndef MPCQ_PLANT_WPE
+#define MPCQ_PLANT_WPE 2
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? MPCQ_PLANT_WPE : 2, NC <= 20 ? 8 : 4))) void plant_step_kernel(PlantStepArgs a)
 {
     static_assert(NC % 4 == 0, "broadcast rows are read 16 B at a time");
     constexpr int LD = NC + 1;
@@ -219,60 +222,69 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 4))) void
             }
             wave_sync();
         }
+        double cab = 0.0;  // Cd Ad^r Bd
         if (lr) {
-            double v = 0.0;
 #pragma unroll
-            for (int s = 0; s < 8; s++) v += Cd[s < nx ? s : 0] * (s < nx ? V[r * 8 + s] : 0.0);
-            S.CAB[r] = v;  // Cd Ad^r Bd
+            for (int s = 0; s < 8; s++) cab += Cd[s < nx ? s : 0] * (s < nx ? V[r * 8 + s] : 0.0);
         }
-        wave_sync();
-        if (r == 0) {
-            double v = 0.0;
-            for (int k = 0; k < N; k++) { v += S.CAB[k]; S.CS[k] = v; }  // Su(i, j) = CS[i - j]
-        }
+        const double cs = psum(cab);  // Su(i, j) = CS[i - j] = sum_{k <= i - j} CAB[k]
+        if (r < NC) S.CS[r] = lr ? cs : 0.0;
         wave_sync();
     }
     const double Q = a.Q[p], R = a.R[p], RD = a.RD[p];
     const double *K = a.K + (size_t)p * nx;
     const double K0 = K[0];
-    // this step's inputs (controllerStep: X, U), read now so the condensing's Fx row is consumed here
+    // this step's inputs (controllerStep: X, U)
     double Xv[8];
     const double *Xp = a.X + (size_t)p * nx;
 #pragma unroll
     for (int c = 0; c < 8; c++) Xv[c] = c < nx ? Xp[c] : 0.0;
     const double Uv = a.U[p];
-    // row r of P (setH :250-251: H1 = 2 (LL' Rbar LL + RbarD + Su' Qbar Su), symmetric as computed, so
-    // (H1 + H1') / 2 = H1), in registers; Fu[r] (:305, incl. the diagonal() quirk: R 1), Fr 1 xref
-    // (:306, :374) and Fx row r (:307) fold straight into q = Fx X + Fu U + Fr ref (setF, :374)
+    // the free response (Sx X)_k = Cd Ad^(k+1) X, lane k: with it q = Fx X + Fu U + Fr 1 xref (setF,
+    // :374; Fx = 2 Su' Qbar Sx, :307) is 2 Q sum_{k >= r} CS[k - r] ((Sx X)_k - xref) + Fu U
+    {
+        double y = 0.0;
+        if (lr) {
+#pragma unroll
+            for (int c = 0; c < 8; c++)
+                if (c < nx) y += Cr[(r + 1) * 8 + c] * Xv[c];
+        }
+        if (r < NC) S.tmp[r] = y;
+    }
+    wave_sync();
+    // P (setH :250-251: H1 = 2 (LL' Rbar LL + RbarD + Su' Qbar Su), symmetric as computed, so
+    // (H1 + H1') / 2 = H1): (Su'Su)(r, j) = sum_{k >= max(r,j)} CS[k - r] CS[k - j] = G(|r - j|, N - 1 -
+    // max(r, j)) with G(d, T) = sum_{t <= T} CS[t] CS[t + d]: lane t forms CS[t] CS[t + d] for every lag
+    // d, one prefix scan per lag gives G(d, .) across the lanes, and lane r gathers its row from LDS
+    // (the recurrences' scratch is dead by now).  Row r stays in registers.
+    double *G = S.Ph;  // G[d][t], stride LD
+    {
+        const double ct = lr ? S.CS[r] : 0.0;
+#pragma unroll
+        for (int d = 0; d < NC; d++) {
+            const int td = r + d < NC ? r + d : NC - 1;
+            const double prod = (lr && r + d < N) ? ct * S.CS[td] : 0.0;
+            const double g = psum(prod);
+            if (r < NC) G[d * LD + r] = g;
+        }
+    }
+    wave_sync();
     double pr[NC];
 #pragma unroll
     for (int j = 0; j < NC; j++) {
         double v = 0.0;
         if (lr && j < N) {
-            const int mx = r > j ? r : j;
-            double t4 = 0.0;
-            for (int k = mx; k < N; k++) t4 += (S.CS[k - r] * Q) * S.CS[k - j];
-            v = 2.0 * ((R * (double)(N - mx) + (r == j ? RD : 0.0)) + t4);
+            const int mx = r > j ? r : j, d = r > j ? r - j : j - r;
+            v = 2.0 * ((R * (double)(N - mx) + (r == j ? RD : 0.0)) + Q * G[d * LD + (N - 1 - mx)]);
         }
         pr[j] = v;
     }
     double qk = 0.0;
     if (lr) {
-        double s1 = 0.0, sf = 0.0;
-        for (int k = r; k < N; k++) {
-            s1 += (S.CS[k] * Q) * S.CS[k - r];
-            sf += -2.0 * (Q * S.CS[k - r]) * a.xref;
-        }
-        const double Fu = 2.0 * (R + s1);
-        double s0 = 0.0;
-#pragma unroll
-        for (int c = 0; c < 8; c++) {
-            double v = 0.0;
-            if (c < nx)
-                for (int k = r; k < N; k++) v += (Cr[(k + 1) * 8 + c] * Q) * S.CS[k - r];
-            if (c < nx) s0 += (2.0 * v) * Xv[c];
-        }
-        qk = s0 + Fu * Uv + sf;
+        const double Fu = 2.0 * (R + Q * G[r * LD + (N - 1 - r)]);  // Fu[r] (:305, incl. the diagonal() quirk: R 1)
+        double f = 0.0;
+        for (int k = r; k < N; k++) f += S.CS[k - r] * (S.tmp[k] - a.xref);
+        qk = (2.0 * Q) * f + Fu * Uv;
     }
     double kx = 0.0;  // K X (Sbar rows < s_rows, :185,208)
 #pragma unroll
@@ -487,12 +499,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 4))) void
         T dyt = T(0), dyb = T(0);
         if (lr && !done) {
             T v = tt_fma(alpha, zz, oma * zt);
-            T zn = __builtin_fmin(tt_fma(rinv, yt, v), ut);
+            T zn = tt_fmin(tt_fma(rinv, yt, v), ut);
             dyt = rho * (v - zn);
             yt = tt_fma(rho, v - zn, yt);
             zt = zn;
             v = tt_fma(alpha, -zz, oma * zb);
-            zn = __builtin_fmin(tt_fma(rinv, yb, v), ub);
+            zn = tt_fmin(tt_fma(rinv, yb, v), ub);
             dyb = rho * (v - zn);
             yb = tt_fma(rho, v - zn, yb);
             zb = zn;

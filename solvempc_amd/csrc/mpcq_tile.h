@@ -57,6 +57,14 @@ template <> __device__ __forceinline__ double tt_fma(double a, double b, double 
 template <typename T> __device__ __forceinline__ T tt_abs(T a) { return a < T(0) ? -a : a; }
 template <typename T> __device__ __forceinline__ T tt_max(T a, T b) { return a > b ? a : b; }
 template <typename T> __device__ __forceinline__ T tt_min(T a, T b) { return a < b ? a : b; }
+// IEEE minNum / maxNum / |x| at the operand's own width (__builtin_fmin & co. are the double builtins:
+// on float operands they widen, compare in fp64 and narrow back)
+__device__ __forceinline__ float tt_fmin(float a, float b) { return __builtin_fminf(a, b); }
+__device__ __forceinline__ double tt_fmin(double a, double b) { return __builtin_fmin(a, b); }
+__device__ __forceinline__ float tt_fmax(float a, float b) { return __builtin_fmaxf(a, b); }
+__device__ __forceinline__ double tt_fmax(double a, double b) { return __builtin_fmax(a, b); }
+__device__ __forceinline__ float tt_fabs(float a) { return __builtin_fabsf(a); }
+__device__ __forceinline__ double tt_fabs(double a) { return __builtin_fabs(a); }
 // max(m, |x|) for the infinity norms (one v_max with an |.| source modifier; equals OSQP's
 // c_max(m, c_absval(x)) for every non-NaN x).
 // min for the projection onto u without LLVM's NaN canonicalisation of the operands (a v_max x, x
@@ -73,7 +81,7 @@ __device__ __forceinline__ double vmin(double a, double b)
     asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
-template <typename T> __device__ __forceinline__ T nrm(T m, T x) { return __builtin_fmax(m, __builtin_fabs(x)); }
+template <typename T> __device__ __forceinline__ T nrm(T m, T x) { return tt_fmax(m, tt_fabs(x)); }
 
 // Reductions over the 4 lanes (groups) of one QP column (lanes c, c+16, c+32, c+48) with the gfx950
 // lane-swap instructions (v_permlane16_swap / v_permlane32_swap: VALU, no LDS round trip).  After a
@@ -111,7 +119,7 @@ template <typename F> __device__ __forceinline__ double col_reduce(double v, F o
 }
 template <typename T> __device__ __forceinline__ T col_max(T v)
 {
-    return col_reduce(v, [](T a, T b) { return __builtin_fmax(a, b); });
+    return col_reduce(v, [](T a, T b) { return tt_fmax(a, b); });
 }
 template <typename T> __device__ __forceinline__ T col_sum(T v)
 {
@@ -760,7 +768,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                     const T zts = s < KN ? zt[gi][s] : -zt[gi][s - KN];
                     const T v = tt_fma(alpha, zts, oma * z[gi][s]);
                     T zn = tt_fma(rij, y[gi][s], v);
-                    zn = __builtin_fmin(zn, uh[gi][s]);
+                    zn = tt_fmin(zn, uh[gi][s]);
                     if (DELTA) dy[gi][s] = rj * (v - zn);
                     y[gi][s] = tt_fma(rj, v - zn, y[gi][s]);
                     z[gi][s] = zn;
@@ -1044,8 +1052,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                     }
                     const T v = tt_fma(alpha, wz[gi][s], oma * z[gi][s]);
                     T zn = tt_fma(rij, y[gi][s], v);
-                    if (!LFREE) zn = __builtin_fmax(zn, lh[gi][s]);  // == OSQP's c_max/c_min, NaN included
-                    zn = __builtin_fmin(zn, uh[gi][s]);
+                    if (!LFREE) zn = tt_fmax(zn, lh[gi][s]);  // == OSQP's c_max/c_min, NaN included
+                    zn = tt_fmin(zn, uh[gi][s]);
                     if (DELTA) dy[gi][s] = rj * (v - zn);  // OSQP delta_y (certificates only)
                     y[gi][s] = tt_fma(rj, v - zn, y[gi][s]);
                     z[gi][s] = zn;

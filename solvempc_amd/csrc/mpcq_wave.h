@@ -49,7 +49,7 @@ template <typename T, typename F> __device__ __forceinline__ T wave_reduce(T v, 
 }
 template <typename T> __device__ __forceinline__ T wmax(T v)
 {
-    return wave_reduce(v, [](T a, T b) { return __builtin_fmax(a, b); });
+    return wave_reduce(v, [](T a, T b) { return tt_fmax(a, b); });
 }
 template <typename T> __device__ __forceinline__ T wsum(T v)
 {
@@ -378,8 +378,8 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
         if (lm) {
             const T v = tt_fma(alpha, zt, oma * z);
             T zn = tt_fma(rij, y, v);
-            if (!LFREE) zn = __builtin_fmax(zn, lh);
-            zn = __builtin_fmin(zn, uh);
+            if (!LFREE) zn = tt_fmax(zn, lh);
+            zn = tt_fmin(zn, uh);
             dy = rj * (v - zn);
             y = tt_fma(rj, v - zn, y);
             z = zn;
@@ -396,12 +396,12 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
         if (lm) {
             const T ax = row_dot(Brow, bcx, T(0));
             const T r = ax - z, ei = Einv_p[lane];
-            ax_z = __builtin_fabs(r);
-            ax_zs = __builtin_fabs(ei * r);
-            zn_r = __builtin_fabs(z);
-            zn_s = __builtin_fabs(ei * z);
-            axn_r = __builtin_fabs(ax);
-            axn_s = __builtin_fabs(ei * ax);
+            ax_z = tt_fabs(r);
+            ax_zs = tt_fabs(ei * r);
+            zn_r = tt_fabs(z);
+            zn_s = tt_fabs(ei * z);
+            axn_r = tt_fabs(ax);
+            axn_s = tt_fabs(ei * ax);
         }
         T dr_r = 0, dr_s = 0, qn_r = 0, qn_s = 0, atyn_r = 0, atyn_s = 0, pxn_r = 0, pxn_s = 0;
         if (ln) {
@@ -409,14 +409,14 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
             px = mem_dot<T, NCAP>(ops + L.PW + (size_t)lane * nc, 1, bcx, px);
             aty = mem_dot<T, MCAP>(ops + L.Ah + lane, nc, bcw, aty);
             const T r = (qh + px) + aty, di = Dinv_p[lane];
-            dr_r = __builtin_fabs(r);
-            dr_s = __builtin_fabs(di * r);
-            qn_r = __builtin_fabs(qh);
-            qn_s = __builtin_fabs(di * qh);
-            atyn_r = __builtin_fabs(aty);
-            atyn_s = __builtin_fabs(di * aty);
-            pxn_r = __builtin_fabs(px);
-            pxn_s = __builtin_fabs(di * px);
+            dr_r = tt_fabs(r);
+            dr_s = tt_fabs(di * r);
+            qn_r = tt_fabs(qh);
+            qn_s = tt_fabs(di * qh);
+            atyn_r = tt_fabs(aty);
+            atyn_s = tt_fabs(di * aty);
+            pxn_r = tt_fabs(px);
+            pxn_s = tt_fabs(di * px);
         }
         ax_z = wmax(ax_z); ax_zs = wmax(ax_zs); zn_s = wmax(zn_s); zn_r = wmax(zn_r);
         axn_s = wmax(axn_s); axn_r = wmax(axn_r);
@@ -434,7 +434,7 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
                 const bool uinf = up > T(kInfty * kMinScaling), linf = lo < T(-kInfty * kMinScaling);
                 if (uinf) d = linf ? T(0) : tt_min(d, T(0));
                 else if (linf) d = tt_max(d, T(0));
-                ndy = __builtin_fabs(scaled_term ? d : ops[L.E + lane] * d);
+                ndy = tt_fabs(scaled_term ? d : ops[L.E + lane] * d);
                 if (up < T(kInfty * kMinScaling)) lhs += up * tt_max(d, T(0));
                 if (lo > T(-kInfty * kMinScaling)) lhs += lo * tt_min(d, T(0));
             }
@@ -446,7 +446,7 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
             wave_sync();
             T atd = T(0);
             if (ln) atd = mem_dot<T, MCAP>(ops + L.Ah + lane, nc, bcw, atd);
-            const T nat = wmax(ln ? __builtin_fabs(scaled_term ? atd : Dinv_p[lane] * atd) : T(0));
+            const T nat = wmax(ln ? tt_fabs(scaled_term ? atd : Dinv_p[lane] * atd) : T(0));
             return nat < eps * ndy;
         };
         auto dual_infeasible = [&](T eps) -> bool {
@@ -461,10 +461,10 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
                 t2 = mem_dot<T, NCAP>(ops + L.PW + (size_t)lane * nc, 1, bcx, t2);
             }
             if (lm) t3 = row_dot(Brow, bcx, T(0));
-            const T ndx = wmax(ln ? __builtin_fabs(scaled_term ? t1 : ops[L.D + lane] * t1) : T(0));
+            const T ndx = wmax(ln ? tt_fabs(scaled_term ? t1 : ops[L.D + lane] * t1) : T(0));
             const T cs = scaled_term ? T(1) : ops[L.cs];
             if (!(ndx > T(kDivisionTol) && qdx < -cs * eps * ndx)) return false;
-            const T npdx = wmax(ln ? __builtin_fabs(scaled_term ? t2 : Dinv_p[lane] * t2) : T(0));
+            const T npdx = wmax(ln ? tt_fabs(scaled_term ? t2 : Dinv_p[lane] * t2) : T(0));
             if (!(npdx < cs * eps * ndx)) return false;
             int viol = 0;
             if (lm) {
