@@ -508,9 +508,10 @@ def main_lti(a, rank, world, local, dist, dev):
                            "frac": ach / PEAK_TFLOPS[a.dtype], "traffic": None,
                            "kernel": "plant_step_kernel (condense + setup + solve, one pass)", "kernel_ms": kern_ms,
                            "flops_per_step": pf,
-                           "flops_note": "as performed (workload.flops_plant_step): condensing, Ruiz, 8N^3 per KKT "
-                                         "inverse (setup + one per rho change), 6N^2 + 20N per iteration (paired "
-                                         "rows), 6N^2 + 30N per check; the fp64 setup is priced at the same peak",
+                           "flops_note": "as performed (workload.flops_plant_step): condensing by lag scans, Ruiz, "
+                                         "2N^3 + 10N^2 per KKT inverse (setup + one per rho change), 4N^2 + 23N per "
+                                         "iteration (A structural: prefix / suffix scans), 2N^2 + 36N per check; the "
+                                         "fp64 setup is priced at the same peak",
                            "dense_equivalent": {"flops_per_step": flops_dense + B * workload.flops_plant_setup(N, 2 * N),
                                                 "note": "SURVEY §8d: dense F_iter / F_check + F_condense + Ruiz + one LDL"}}
         rec["iters"]["rho_adapted_frac"] = float(refac.mean())

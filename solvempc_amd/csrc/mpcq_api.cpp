@@ -78,6 +78,8 @@ struct mpcq_ctx {
     // OneShot: mpcq_mpc_plants_step_device left this step's results but no operators behind.
     enum class Mode { None, Generic, Mimo, OneShot } mode = Mode::None;
     bool all_ineq = true, mpc_ready = false, lower_free = false, fresh = false;
+    double dinf_ks = 0.0, dinf_ku = 0.0;  // dual-infeasibility bounds (AdmmArgs::dinf_kappa), 0: none
+    int cus = 256;                        // compute units of the device (phase lists)
     bool paired = false;  // shared plant of the condensed-MPC shape (tile kernel's paired loop)
     bool inv_ops = false; // per-plant operators in the direct-inverse reading (setup_inv_kernel): wave kernel only
     // tile (MFMA) path: shared plant with a compiled (KN, KM) shape
@@ -184,6 +186,7 @@ mpcq::AdmmArgs<T> make_args(mpcq_ctx *c)
     const int ct = c->set.check_termination;
     a.adaptive_interval = c->set.adaptive_rho_interval ? c->set.adaptive_rho_interval : (ct ? 4 * ct : 100);
     a.all_ineq = c->all_ineq;
+    a.dinf_kappa = c->set.scaled_termination ? c->dinf_ks : c->dinf_ku;
     a.lower_free = c->lower_free;
     a.q = c->d_q;
     a.u = c->d_u;
@@ -357,6 +360,7 @@ int mpcq_create(const mpcq_dims *d, const mpcq_settings *s, mpcq_ctx **out)
     c->set = st;
     c->nc = nc;
     c->mc = mc;
+    c->cus = prop.multiProcessorCount;
     c->tile = tile;
     c->mimo_only = !tile && (d->n > 32 || d->m > 64);
     c->KN = KN;
@@ -430,6 +434,30 @@ int mpcq_destroy(mpcq_ctx *c)
         if (p) (void)hipFree(p);
     delete c;
     return MPCQ_OK;
+}
+
+// Lower bounds kappa on ||P^ dx|| / ||dx|| in the two norms OSQP's is_dual_infeasible compares
+// (AdmmArgs::dinf_kappa), for a shared plant in the eigen-basis with every row an inequality: then
+// P~ = P^ + sigma I and W' P~ W = I, so lambda_min(P~) = 1 / ||W||_2^2 >= 1 / ||W||_F^2 and
+// mu = 1 / ||W||_F^2 - sigma <= lambda_min(P^).  With v = dx (scaled space):
+//   ||P^ v||_inf >= mu ||v||_2 / sqrt(n) >= (mu / sqrt(n)) ||v||_inf                     (scaled_termination)
+//   ||D^-1 P^ v||_inf >= (min_i D_i^-1) (mu / sqrt(n)) ||v||_inf
+//                     >= (min_i D_i^-1) mu / (sqrt(n) max_i D_i) ||D v||_inf              (unscaled)
+static void dinf_bounds(mpcq_ctx *c, const double *blk, const mpcq::OpsLayout &L)
+{
+    c->dinf_ks = c->dinf_ku = 0.0;
+    const size_t n = c->dims.n;
+    if (c->dims.n_plants != 1 || c->inv_ops || !c->all_ineq || n == 0) return;
+    double fro = 0.0, dmax = 0.0, dinv_min = HUGE_VAL;
+    for (size_t i = 0; i < (size_t)c->nc * c->nc; i++) fro += blk[L.W + i] * blk[L.W + i];
+    for (size_t i = 0; i < n; i++) {
+        dmax = std::max(dmax, blk[L.D + i]);
+        dinv_min = std::min(dinv_min, 1.0 / blk[L.D + i]);
+    }
+    const double mu = 1.0 / fro - c->set.sigma;
+    if (!(fro > 0.0) || !(mu > 0.0) || !(dmax > 0.0)) return;
+    c->dinf_ks = mu / std::sqrt((double)n);
+    c->dinf_ku = dinv_min * mu / (std::sqrt((double)n) * dmax);
 }
 
 // Setup kernels on the device-resident setup data (d_P, d_q0, d_A, d_l0, d_u0), operator
@@ -512,6 +540,7 @@ int setup_on_device(mpcq_ctx *c, hipStream_t s)
     for (size_t i = 0; i < n; i++) c->hD[i] = blk[L.D + i];
     for (size_t j = 0; j < m; j++) c->hE[j] = blk[L.E + j];
     c->hc = blk[L.cs];
+    dinf_bounds(c, blk.data(), L);
     if (c->dims.dtype == MPCQ_F32 &&
         mpcq_internal_f64_to_f32(c->d_ops, c->d_ops32, Pn * c->ops_stride, s) != 0)
         return fail(MPCQ_ERR_HIP, "operator conversion failed");
@@ -618,14 +647,23 @@ int mpcq_warm_start(mpcq_ctx *c, const double *x, const double *y)
 }  // extern "C"
 
 // Phase boundaries of the tile path (multiples of check_termination, then max_iter): QPs still
-// running at a boundary are re-packed densely into the waves of the next launch.
-static int phase_stops(const mpcq_settings &st, int *stops)
+// running at a boundary are re-packed densely into the waves of the next launch.  One boundary at
+// 4 check_termination (100 iterations at the defaults; a second one at 3 when the batch is more than
+// ~1.5 rounds of the chip's tile-wave slots, where the re-pack at 75 pays), then one launch to
+// max_iter: the few QPs that need more than ~125 iterations finish in their (mostly idle) tile waves,
+// which beats a one-QP-per-wave launch for them (its prologue and a hand-off through HBM).
+static int phase_stops(const mpcq_settings &st, int batch, int cus, int *stops)
 {
     const int ct = st.check_termination;
     int np = 0;
     const char *e = test_hook("MPCQ_PHASES");  // "0" = one launch per solve, or check multiples "3,4,5"
-    int mult[kMaxPhases] = {3, 4, 5, 6, 8, 12, 20, 40, 80, 160};
-    int nm = 10;
+    const bool many = (long)batch / 16 > (long)cus * 4 * 3 * 3 / 2;  // waves vs 3 waves/SIMD, 4 SIMD/CU
+    int mult[kMaxPhases] = {3, 4};
+    int nm = 2;
+    if (!many) {
+        mult[0] = 4;
+        nm = 1;
+    }
     const int cap = kMaxPhases;
     if (e[0] == '0') nm = 0;
     else if (*e) {
@@ -665,7 +703,7 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
 {
     const int B = c->dims.batch;
     int stops[kMaxPhases];
-    const int np = phase_stops(c->set, stops);
+    const int np = phase_stops(c->set, B, c->cus, stops);
     const int seg = mpcq::ListSeg::cap(B);
     const size_t lcap = (size_t)mpcq::ListSeg::kShards * seg;
     // Counter blocks: launch p zeroes block p + 1 (its successor's output) and a chain's final launch,
@@ -675,7 +713,7 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
         return -2;
     c->count0_clean = false;
     const int mpc = a.mpc;
-    const int tail_from = wave_only ? 0 : 3;  // from the fourth launch on one QP per wave
+    const int tail_from = wave_only ? 0 : kMaxPhases;  // one QP per wave: small batches only
     int np_run = 0;
     a.list_seg = seg;
 

@@ -181,6 +181,11 @@ struct AdmmArgs {
     int stop_iter;              // phase boundary (multiple of check_termination, or max_iter)
     int resume;                 // 1: phase >= 2 (state, rho and iteration count come from the buffers)
     long long *stamps;          // debug build (MPCQ_DEBUG_HOOKS): [wave][8] s_memtime stamps, or null
+    // OSQP is_dual_infeasible needs ||P^ dx|| < c eps ||dx|| (norms as the termination mode reads them);
+    // with lambda_min(P^) >= mu > 0 the left side is >= kappa ||dx|| (kappa from mu, D and n: host,
+    // setup_on_device), so for kappa > 2 c eps the certificate cannot hold and its products are skipped
+    // (0: always evaluated)
+    double dinf_kappa;
 };
 
 // MFMA operand images of one shared plant for the tile kernel (mpcq_tile.h).  A vector of length

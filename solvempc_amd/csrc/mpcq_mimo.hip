@@ -140,7 +140,7 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
     double *P = sm + S.P, *Ad = sm + S.Ad, *Bd = sm + S.Bd, *Cd = sm + S.Cd, *Q = sm + S.Q, *R = sm + S.R;
     double *RD = sm + S.RD, *K0 = sm + S.K0, *AB = sm + S.AB, *CA = sm + S.CA, *CS = sm + S.CS, *QCS = sm + S.QCS;
     double *Dv = sm + S.Dv, *Ev = sm + S.Ev, *Dt = sm + S.Dt, *Et = sm + S.Et, *cm = sm + S.cm, *wk = sm + S.wk;
-    double *red = sm + S.red, *sh = sm + S.sh;
+    double *red = sm + S.red;
     const MimoLayout L = MimoLayout::make(N, nx, nu, ny);
     double *out = a.ops + (size_t)pl * L.total;
 #define MPCQ_SSTAMP(k)                                                                              \
@@ -462,7 +462,6 @@ constexpr int kSegLd = 18;                  // padded stride of a 16-element seg
 constexpr int kSegN = 8 * kSegLd;
 __device__ __forceinline__ int seg_of(int i) { return i + 2 * (i >> 4); }
 constexpr int kMimoN = 128;       // n capacity
-constexpr int kMimoBlk = 64 * 4;  // block-major vector slots: lane k, component c at 4 k + c
 
 struct B4 {
     double v[4];

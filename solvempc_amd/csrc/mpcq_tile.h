@@ -1223,6 +1223,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
         };
         // OSQP is_dual_infeasible on delta_x^ = W dx, per group.
         auto dual_infeasible = [&](T eps, const bool (&need)[G], bool (&res)[G]) {
+            if (a.dinf_kappa > 2.0 * (scaled_term ? 1.0 : c64) * (double)eps) {  // cannot hold (AdmmArgs)
+#pragma unroll
+                for (int gi = 0; gi < G; gi++) res[gi] = false;
+                return;
+            }
             T qdx[G];
             bool cand[G], anyc = false;
 #pragma unroll

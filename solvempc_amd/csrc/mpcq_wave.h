@@ -450,6 +450,7 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
             return nat < eps * ndy;
         };
         auto dual_infeasible = [&](T eps) -> bool {
+            if (a.dinf_kappa > 2.0 * (scaled_term ? 1.0 : (double)ops[L.cs]) * (double)eps) return false;  // (AdmmArgs)
             const T qdx = wsum(ln ? -gk * dx : T(0));  // q^' dx^ = (W' q^)' dx'
             if (!(qdx < T(0))) return false;
             wave_sync();

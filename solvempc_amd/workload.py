@@ -173,18 +173,22 @@ def flops_plant_setup(n: int, m: int, N: int | None = None) -> float:
 
 
 def flops_plant_step(N: int, nx: int, iters, refactors, scaling: int = 10, check: int = 25) -> np.ndarray:
-    """FLOPs plant_step_kernel performs per plant (mpcq_plant.hip; FMA = 2, m = 2N with the paired rows):
-    condensing (the Ad^k Bd / Cd Ad^k recurrences 4 N nx^2, CAB 2 N nx, P rows ~N^3, Fu / Fr 1 / Fx
-    ~(6 + 2 nx) N^2 / 2), Ruiz (`scaling` passes over P and the N x N half of A: ~7 N^2 each), the KKT
-    matrix 4 N^3 and its Gauss-Jordan inverse 2 N^3 plus (A^ M^-1) 2 N^3 at setup and at every
-    refactorisation, the front end 2 N (nx + 2), and per iteration the three N x N products 6 N^2 plus
-    ~20 N element-wise, per check three more products 6 N^2 and ~30 N of norms."""
+    """FLOPs plant_step_kernel performs per plant (mpcq_plant.hip; FMA = 2, m = 2N with the paired rows,
+    A = [K0 L; -K0 L] applied structurally):
+    * condensing: the Ad^k Bd / Cd Ad^k recurrences 4 N nx^2, CAB and the free response 4 N nx, the
+      per-lag products and prefix scans of the Hessian 2 N^2, P rows and q ~4 N^2;
+    * Ruiz, `scaling` passes: P's row norms and scaling ~4 N^2, the structural A norms (scans) ~4 N;
+    * per factorisation (setup + every refactorisation): M(rho) ~4 N^2, Gauss-Jordan 2 N^3, g = -M^-1 q
+      2 N^2, the (A^ M^-1) columns by prefix sums 4 N^2;
+    * front end 2 N (nx + 2);
+    * per iteration: sigma M^-1 x and (A^ M^-1)' w, 4 N^2, the A^ x~ prefix scan ~3 N, ~20 N element-wise;
+    * per check: P^ x 2 N^2, the A^ x and A^'y scans ~6 N, ~30 N of residuals and norms (fp64)."""
     it = np.asarray(iters, dtype=np.float64)
-    cond = 4 * N * nx * nx + 2 * N * nx + N ** 3 + (6 + 2 * nx) * N * N / 2
-    ruiz = scaling * 7 * N * N
-    kkt = 8 * N ** 3
+    cond = 4 * N * nx * nx + 4 * N * nx + 6 * N * N
+    ruiz = scaling * (4 * N * N + 4 * N)
+    kkt = 2 * N ** 3 + 10 * N * N
     return (cond + ruiz + 2 * N * (nx + 2) + (1 + np.asarray(refactors, dtype=np.float64)) * kkt
-            + it * (6 * N * N + 20 * N) + np.floor(it / check) * (6 * N * N + 30 * N))
+            + it * (4 * N * N + 23 * N) + np.floor(it / check) * (2 * N * N + 36 * N))
 
 
 # ----------------------------------------------------------------------------- config 4: quad-rotor
