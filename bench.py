@@ -315,6 +315,21 @@ def traffic_per_solve(dtype, batch, N):
     return d.get("bytes_per_solve")
 
 
+def mfma_util(dtype, kernel="admm_tile_kernel"):
+    """MFMA utilisation of the dominant kernel from the committed PMC pass (tools/pmc.sh +
+    tools/pmc_mfma.py -> profiles/pmc_mfma_<dtype>.json: SQ_VALU_MFMA_BUSY_CYCLES over SIMD-cycles), or
+    None.  A recorded measurement of the same bench command, not re-measured by this run."""
+    f = ROOT / "profiles" / f"pmc_mfma_{dtype}.json"
+    try:
+        d = json.loads(f.read_text()).get(kernel, {})
+    except (OSError, ValueError):
+        return None
+    if "mfma_util" not in d:
+        return None
+    return {"value": d["mfma_util"], "source": f"profiles/{f.name} (rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES, "
+                                              f"GRBM_GUI_ACTIVE; bench.py --steps 3 --warmup 1)"}
+
+
 def main_dry(a, rank, world, dist):
     """--dry-run: the launcher, the rendezvous and the per-step gather of the applied moves on the
     CPU (gloo), no device work.  value is null: nothing is solved."""
@@ -480,6 +495,7 @@ def main_lti(a, rank, world, local, dist, dev):
     rec["roofline"] = {
         "bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS[a.dtype], "unit": "TFLOP/s",
         "frac": achieved / PEAK_TFLOPS[a.dtype], "traffic": traffic_per_solve(a.dtype, B, N) if not stream_mode else None,
+        "mfma_util": mfma_util(a.dtype) if a.workload == "cfg2" and B == 65536 else None,
         "kernel": f"admm_{kind}_kernel{' (paired loop)' if paired else ''} (all launches of "
                   f"{'the step' if not stream_mode else 'the control steps'})",
         "kernel_ms": kern_ms, "flops_per_step": flops,

@@ -1,11 +1,12 @@
 #!/bin/bash
 # PMC passes over a short bench run (one rocprofv3 run per counter set; never combined with tracing).
-#   usage (on the GPU box): bash tools/pmc.sh <dtype> <outdir>
+#   usage (on the GPU box): bash tools/pmc.sh <dtype> <outdir>   (CMD=... overrides the profiled program,
+#   PMC_SETS=... the counter passes, one line each)
 cd "$GRAFT_REPO_ROOT" || exit 2
 export TMPDIR=/tmp
 dt=${1:-f32}; out=${2:-gpurun_out/pmc_$dt}
 mkdir -p "$out"
-CMD="python bench.py --steps 3 --warmup 1 --dtype $dt --cpu-seconds 0"
+CMD=${CMD:-"python bench.py --steps 3 --warmup 1 --dtype $dt --cpu-seconds 0"}
 i=0
 while read -r set; do
   [ -z "$set" ] && continue
