@@ -80,6 +80,12 @@ struct mpcq_ctx {
     bool all_ineq = true, mpc_ready = false, lower_free = false, fresh = false;
     double dinf_ks = 0.0, dinf_ku = 0.0;  // dual-infeasibility bounds (AdmmArgs::dinf_kappa), 0: none
     int cus = 256;                        // compute units of the device (phase lists)
+    // A tile-path controllerStep leaves q, u (the solver's data after updateGradient / updateUpperBound)
+    // as the step's saved X, U: d_q, d_u are filled from them by materialize_qu before anything reads
+    // them (a generic solve, the device view, an update, new operators).
+    double *d_Xs = nullptr, *d_Us = nullptr;
+    bool qu_lazy = false;
+    double lazy_xref = 0.0;
     bool paired = false;  // shared plant of the condensed-MPC shape (tile kernel's paired loop)
     bool inv_ops = false; // per-plant operators in the direct-inverse reading (setup_inv_kernel): wave kernel only
     // tile (MFMA) path: shared plant with a compiled (KN, KM) shape
@@ -427,7 +433,7 @@ int mpcq_destroy(mpcq_ctx *c)
                     c->d_xs, c->d_zs, c->d_ys, c->d_rhos, c->d_snx, c->d_sny, c->d_Fx, c->d_Fu, c->d_Fr,
                     c->d_Sbar, c->d_Ku, c->d_W0, c->d_X, c->d_U, c->d_img, c->d_list, c->d_counts,
                     c->d_itstate, c->d_Ad, c->d_Bd, c->d_step, c->d_flags, c->d_stamps, c->d_mimo,
-                    c->d_it_acc, c->d_uns_acc};
+                    c->d_it_acc, c->d_uns_acc, c->d_Xs, c->d_Us};
     if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
     if (c->graph) (void)hipGraphDestroy(c->graph);
     for (void *p : ptrs)
@@ -465,6 +471,7 @@ static void dinf_bounds(mpcq_ctx *c, const double *blk, const mpcq::OpsLayout &L
 // readback.  One 4-byte flag word (non-convex plant, non-inequality row) comes back to the host.
 int setup_on_device(mpcq_ctx *c, hipStream_t s)
 {
+    c->qu_lazy = false;  // (q, u are re-broadcast from the setup data below)
     c->gen++;
     const size_t Pn = c->dims.n_plants, n = c->dims.n, m = c->dims.m, B = c->dims.batch;
     HIPCHK(hipMemsetAsync(c->d_ops, 0, 8 * Pn * c->ops_stride, s));
@@ -582,10 +589,13 @@ int mpcq_setup(mpcq_ctx *c, const double *P, const double *q0, const double *A, 
     return MPCQ_OK;
 }
 
+static int materialize_qu(mpcq_ctx *c);  // (below: the lazy q, u of a tile-path controllerStep)
+
 int mpcq_update_lin_cost(mpcq_ctx *c, const double *q)
 {
     int rc = check_ctx(c, kGeneric);
     if (rc) return rc;
+    if ((rc = materialize_qu(c))) return rc;  // (the other vector of the pending step)
     if (!q) return fail(MPCQ_ERR_ARG, "null q");
     return h2d(c->d_q, q, 8 * (size_t)c->dims.batch * c->dims.n, c->last);
 }
@@ -594,6 +604,7 @@ int mpcq_update_upper_bound(mpcq_ctx *c, const double *u)
 {
     int rc = check_ctx(c, kGeneric);
     if (rc) return rc;
+    if ((rc = materialize_qu(c))) return rc;  // (the other vector of the pending step)
     if (!u) return fail(MPCQ_ERR_ARG, "null u");
     return h2d(c->d_u, u, 8 * (size_t)c->dims.batch * c->dims.m, c->last);
 }
@@ -602,6 +613,7 @@ int mpcq_update_lower_bound(mpcq_ctx *c, const double *l)
 {
     int rc = check_ctx(c, kGeneric);
     if (rc) return rc;
+    if ((rc = materialize_qu(c))) return rc;  // (the other vector of the pending step)
     if (!l) return fail(MPCQ_ERR_ARG, "null l");
     const bool lf = lower_all_free_batch(c, l);
     if (lf != c->lower_free) c->gen++;
@@ -815,7 +827,14 @@ static int launch_typed(mpcq_ctx *c, hipStream_t s, bool mpc, const double *X, d
     if (mpc) {
         a.mpc = 1; a.mpc_u = 1; a.nx = c->nx; a.X = X; a.U = U; a.xref = xref;
         a.Fx = c->d_Fx; a.Fu = c->d_Fu; a.Fr = c->d_Fr; a.Sbar = c->d_Sbar; a.Ku = c->d_Ku; a.W0 = c->d_W0;
-        a.q_out = c->d_q; a.u_out = c->d_u;
+        const bool lazy = c->tile && choose_path(c).kind == MPCQ_PATH_TILE && c->d_Xs && c->d_Us;
+        if (lazy) {  // phase 0 saves X, U (40 B/QP) instead of writing q, u (480 B/QP): materialize_qu
+            a.X_save = c->d_Xs; a.U_save = c->d_Us;
+        } else {
+            a.q_out = c->d_q; a.u_out = c->d_u;
+        }
+        c->qu_lazy = lazy;
+        c->lazy_xref = xref;
     }
     return launch_args<T>(c, a, s);
 }
@@ -844,6 +863,7 @@ int mpcq_solve(mpcq_ctx *c, void *stream)
 {
     int rc = check_ctx(c, kGeneric);
     if (rc) return rc;
+    if ((rc = materialize_qu(c))) return rc;
     return launch_solve(c, (hipStream_t)stream, false, nullptr, nullptr, 0.0);
 }
 
@@ -903,6 +923,8 @@ int mpcq_get_path(mpcq_ctx *c, int *kind, int *paired)
 int mpcq_device_view_get(mpcq_ctx *c, mpcq_device_view *v)
 {
     if (!c || !v) return fail(MPCQ_ERR_ARG, "null argument");
+    const int rc = materialize_qu(c);  // (enqueued on the context's last stream)
+    if (rc) return rc;
     v->q = c->d_q;
     v->u = c->d_u;
     v->l = c->d_l;
@@ -923,13 +945,27 @@ bool alloc_mpc_ops(mpcq_ctx *c, int nx)
         for (double **p : {&c->d_Fx, &c->d_Sbar})
             if (*p) { (void)hipFree(*p); *p = nullptr; }
         if (c->d_X) { (void)hipFree(c->d_X); c->d_X = nullptr; }
+        if (c->d_Xs) { (void)hipFree(c->d_Xs); c->d_Xs = nullptr; }
     }
     auto A = [&](double **p, size_t cnt) -> bool {
         return *p || hipMalloc((void **)p, 8 * std::max<size_t>(cnt, 1)) == hipSuccess;
     };
     return A(&c->d_Fx, Pn * n * nx) && A(&c->d_Fu, Pn * n) && A(&c->d_Fr, Pn * n * n) &&
            A(&c->d_Sbar, Pn * m * nx) && A(&c->d_Ku, Pn * m) && A(&c->d_W0, Pn * m) &&
-           A(&c->d_X, (size_t)c->dims.batch * nx) && A(&c->d_U, (size_t)c->dims.batch);
+           A(&c->d_X, (size_t)c->dims.batch * nx) && A(&c->d_U, (size_t)c->dims.batch) &&
+           A(&c->d_Xs, (size_t)c->dims.batch * nx) && A(&c->d_Us, (size_t)c->dims.batch);
+}
+
+// d_q, d_u from the last tile-path controllerStep's saved X, U (mpcq_internal_front_end), once.
+static int materialize_qu(mpcq_ctx *c)
+{
+    if (!c->qu_lazy) return MPCQ_OK;
+    c->qu_lazy = false;
+    if (mpcq_internal_front_end((int)c->dims.batch, c->nx, (int)c->dims.n, (int)c->dims.m, c->d_Xs, c->d_Us,
+                                c->lazy_xref, c->d_Fx, c->d_Fu, c->d_Fr, c->d_Sbar, c->d_Ku, c->d_W0, c->d_q,
+                                c->d_u, c->last) != 0)
+        return fail(MPCQ_ERR_HIP, "front-end kernel launch failed");
+    return MPCQ_OK;
 }
 
 int mpcq_mpc_set_operators(mpcq_ctx *c, int nx, const double *Fx, const double *Fu, const double *Fr,
@@ -941,6 +977,7 @@ int mpcq_mpc_set_operators(mpcq_ctx *c, int nx, const double *Fx, const double *
     if (nx <= 0 || nx > 8) return fail(MPCQ_ERR_ARG, "nx must be in 1..8");
     if (m != 2 * n) return fail(MPCQ_ERR_ARG, "MPC front end needs m == 2n (ModelPredictiveControlAPI.cpp:47-48)");
     if (!Fx || !Fu || !Fr || !Sbar || !Ku || !W0) return fail(MPCQ_ERR_ARG, "null operator");
+    if ((rc = materialize_qu(c))) return rc;  // (with the operators the pending step used)
     if (!alloc_mpc_ops(c, nx)) return fail(MPCQ_ERR_HIP, "hipMalloc failed");
     c->nx = nx;
     hipStream_t s = c->last;
@@ -1156,6 +1193,7 @@ int mpcq_mpc_setup_plants_device(mpcq_ctx *c, int nx, int s_rows, const double *
     if (nx <= 0 || nx > 8 || s_rows < 0) return fail(MPCQ_ERR_ARG, "setup_plants: 1 <= nx <= 8, s_rows >= 0");
     if (m != 2 * n) return fail(MPCQ_ERR_ARG, "MPC front end needs m == 2n (ModelPredictiveControlAPI.cpp:47-48)");
     if (!Ad || !Bd || !Cd || !K || !Q || !R || !RD) return fail(MPCQ_ERR_ARG, "setup_plants: null plant array");
+    if ((rc = materialize_qu(c))) return rc;  // (with the operators the pending step used)
     if (!alloc_mpc_ops(c, nx)) return fail(MPCQ_ERR_HIP, "hipMalloc failed");
     c->nx = nx;
     c->mode = mpcq_ctx::Mode::None;

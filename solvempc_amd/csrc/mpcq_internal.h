@@ -165,6 +165,7 @@ struct AdmmArgs {
     int mpc, nx;
     const double *X, *Fx, *Fu, *Fr, *Sbar, *Ku, *W0;
     double *U, *q_out, *u_out;
+    double *X_save, *U_save;    // tile path: phase 0 saves X [batch][nx], U [batch] (q, u computed on demand)
     double xref;
     int mpc_u;                  // U += x[0] at termination (the front end may have run in an earlier phase)
     // tile kernel (shared plant): MFMA operand images and the phase machinery (mpcq_tile.h)
@@ -345,6 +346,9 @@ int mpcq_internal_simulate(int batch, int nx, int shared, const double *Ad, cons
                            const double *U, unsigned long long seed, long long first_qp, const long long *step_p,
                            long long step_v, double noise_std, hipStream_t s);
 int mpcq_internal_tick(long long *step, hipStream_t s);
+int mpcq_internal_front_end(int batch, int nx, int n, int m, const double *Xs, const double *Us, double xref,
+                            const double *Fx, const double *Fu, const double *Fr, const double *Sbar,
+                            const double *Ku, const double *W0, double *q, double *u, hipStream_t s);
 int mpcq_internal_set_step(long long *step, long long v, hipStream_t s);
 // MIMO condensed MPC (mpcq_mimo.hip): per-plant condensing + Ruiz + P^, then the per-QP solve
 // (one 512-thread workgroup per QP: KKT inverse by Gauss-Jordan in VGPRs, structured A).

@@ -83,3 +83,53 @@ extern "C" int mpcq_internal_tick(long long *step, hipStream_t s)
     hipLaunchKernelGGL(mpcq::tick_kernel, dim3(1), dim3(1), 0, s, step);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// The QP data a controllerStep leaves in the solver (OSQP's q and u after updateGradient /
+// updateUpperBound, :96-99), computed from the step's saved X and U when a caller first reads them
+// (mpcq_api.cpp materialize_qu): the tile path's phase 0 saves X, U instead of writing the 480 B/QP
+// fp64 q, u.  The arithmetic is the tile kernel prologue's, operation for operation (fp64, no
+// contraction): q = Fx X + Fu U + (Fr 1 xref), u = W0 + Sbar X + Ku U.
+namespace mpcq {
+__global__ void front_end_kernel(int batch, int nx, int n, int m, const double *Xs, const double *Us, double xref,
+                                 const double *Fx, const double *Fu, const double *Fr, const double *Sbar,
+                                 const double *Ku, const double *W0, double *q, double *u)
+{
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int rows = n + m;
+    if (i >= (long long)batch * rows) return;
+    const int b = (int)(i / rows), v = (int)(i % rows);
+    double Xv[8];
+#pragma unroll
+    for (int t = 0; t < 8; t++) Xv[t] = t < nx ? Xs[(size_t)b * nx + t] : 0.0;
+    const double Uv = Us[b];
+    if (v < n) {
+        double s2 = 0.0;  // Fr ref, ref = xref 1 (updateRef :378-380), row sum in order
+        for (int t = 0; t < n; t++) s2 += Fr[(size_t)v * n + t] * xref;
+        double s0 = 0.0;
+#pragma unroll
+        for (int t = 0; t < 8; t++)
+            if (t < nx) s0 += Fx[(size_t)v * nx + t] * Xv[t];
+        const double s1 = Fu[v] * Uv;
+        q[(size_t)b * n + v] = s0 + s1 + s2;
+    } else {
+        const int r = v - n;
+        double sx = 0.0;
+#pragma unroll
+        for (int t = 0; t < 8; t++)
+            if (t < nx) sx += Sbar[(size_t)r * nx + t] * Xv[t];
+        u[(size_t)b * m + r] = W0[r] + sx + Ku[r] * Uv;
+    }
+}
+}  // namespace mpcq
+
+extern "C" int mpcq_internal_front_end(int batch, int nx, int n, int m, const double *Xs, const double *Us, double xref,
+                                       const double *Fx, const double *Fu, const double *Fr, const double *Sbar,
+                                       const double *Ku, const double *W0, double *q, double *u, hipStream_t s)
+{
+    if (nx < 1 || nx > 8) return -1;
+    const long long total = (long long)batch * (n + m);
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(mpcq::front_end_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, batch, nx, n, m, Xs,
+                       Us, xref, Fx, Fu, Fr, Sbar, Ku, W0, q, u);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}

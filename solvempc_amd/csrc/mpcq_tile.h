@@ -420,11 +420,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                   FE_W0 = 10 * NCP + 9 * MCP, FE_E = 10 * NCP + 10 * MCP, FE_D = 10 * NCP + 11 * MCP,
                   FE_TOT = 11 * NCP + 11 * MCP;
     __shared__ double fe[FE_TOT];
+    // (an MPC step: every phase builds q, u from X, U; phase 0 also publishes them or saves X, U)
+    const bool fe_on = a.X != nullptr;
     {
-        const int n = a.n, m = a.m, nx = a.mpc ? a.nx : 0;
+        const int n = a.n, m = a.m, nx = fe_on ? a.nx : 0;
         for (int i = threadIdx.x; i < MCP; i += NTH) fe[FE_E + i] = i < m ? (double)a.ops.E[i] : 0.0;
         for (int i = threadIdx.x; i < NCP; i += NTH) fe[FE_D + i] = i < n ? (double)a.ops.D[i] : 0.0;
-        if (a.mpc) {
+        if (fe_on) {
             for (int i = threadIdx.x; i < 8 * NCP; i += NTH) {
                 const int v = i >> 3, t = i & 7;
                 fe[FE_FX + i] = (v < n && t < nx) ? a.Fx[(size_t)v * nx + t] : 0.0;
@@ -502,7 +504,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     for (int gi = 0; gi < G; gi++) {
         const int b = b_[gi];
         double qk[KN], up[KM], lo[LFREE ? 1 : KM];
-        if (mpc_fe) {  // setF (:372-375) q = Fx X + Fu U + Fr ref;  (:93-99) u = W0 + Sbar X + Ku U
+        if (fe_on) {  // setF (:372-375) q = Fx X + Fu U + Fr ref;  (:93-99) u = W0 + Sbar X + Ku U
+            // (a resumed phase recomputes them: X is read-only and U changes only at a QP's finalize)
             double Xv[8];
             const int nx = a.nx;
 #pragma unroll
@@ -520,7 +523,12 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                     if (t < nx) s0 += fe[FE_FX + 8 * v + t] * Xv[t];
                 const double s1 = fe[FE_FU + v] * Uv;
                 qk[s] = s0 + s1 + fe[FE_FR + v];
-                if (valid[gi] && v < n) a.q_out[(size_t)b * n + v] = qk[s];  // read by later phases
+                if (mpc_fe && a.q_out && valid[gi] && v < n) a.q_out[(size_t)b * n + v] = qk[s];
+            }
+            if (mpc_fe && a.X_save && valid[gi]) {  // the step's X, U: q, u on demand (materialize_qu)
+                if (g < nx) a.X_save[(size_t)b * nx + g] = a.X[(size_t)b * nx + g];  // (cache-hot reloads:
+                if (g + 4 < nx) a.X_save[(size_t)b * nx + g + 4] = a.X[(size_t)b * nx + g + 4];  // no register index by lane)
+                if (g == 0) a.U_save[b] = Uv;
             }
             MPCQ_PRO_MARK(11);
 #pragma unroll
@@ -531,7 +539,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 for (int t = 0; t < 8; t++)
                     if (t < nx) sx += fe[FE_SB + 8 * v + t] * Xv[t];
                 up[s] = fe[FE_W0 + v] + sx + fe[FE_KU + v] * Uv;
-                if (valid[gi] && v < m) a.u_out[(size_t)b * m + v] = up[s];
+                if (mpc_fe && a.u_out && valid[gi] && v < m) a.u_out[(size_t)b * m + v] = up[s];
             }
             MPCQ_PRO_MARK(12);
         } else {

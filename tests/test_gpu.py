@@ -715,6 +715,55 @@ def test_paired_tile_path_selected(plant):
     assert s3.path() == ("wave", False)
 
 
+class _DevArray:
+    """A device buffer of the C ABI's device view, wrapped for torch (__cuda_array_interface__)."""
+
+    def __init__(self, ptr, shape):
+        self.__cuda_array_interface__ = {"shape": shape, "typestr": "<f8", "data": (ptr, False), "version": 3}
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_tile_step_leaves_reference_qp_data(plant, dtype):
+    """A tile-path controllerStep saves X and U; the solver's q and u (what updateGradient /
+    updateUpperBound leave in OSQP, ModelPredictiveControlAPI.cpp:96-99) are computed from them when
+    first read.  The device view must show the step's q, u bit-identical to an eager one-QP-per-wave
+    step (same fp64 arithmetic), within 1e-12 of the oracle's; a generic solve after the step must
+    solve that same QP (statuses and iterations of the step's solve, warm-started from its state)."""
+    import torch
+
+    N, B = 20, 8192
+    ops, X, U, q, u = _problem(plant, N, B, seed=41)
+    dev = torch.device("cuda:0")
+    res = {}
+    for kern in ("tile", "wave"):
+        os.environ["MPCQ_KERNEL"] = kern
+        try:
+            s = sm.BatchSolver(N, 2 * N, B, dtype=dtype)
+            s.setup(ops["P"], np.zeros(N), ops["A"], np.full(2 * N, LMIN), ops["W0"])
+            s.mpc_set_operators(ops["Fx"], ops["Fu"], ops["Fr"], ops["Sbar"], ops["Ku"], ops["W0"])
+            Xd = torch.from_numpy(X).to(dev)
+            Ud = torch.from_numpy(U).to(dev)
+            s.mpc_step_device(Xd.data_ptr(), Ud.data_ptr(), plant["xref"], torch.cuda.current_stream(dev).cuda_stream)
+            assert s.path()[0] == kern
+            v = s.device_view()
+            torch.cuda.synchronize()
+            qd = torch.as_tensor(_DevArray(v["q"], (B, N)), device=dev).cpu().numpy().copy()
+            ud = torch.as_tensor(_DevArray(v["u"], (B, 2 * N)), device=dev).cpu().numpy().copy()
+            res[kern] = (qd, ud, *s.info())
+            if kern == "tile":  # a generic solve of the step's QP from the step's state
+                st0, it0 = s.info()[:2]
+                s.solve()
+                st1, it1 = s.info()[:2]
+                assert np.array_equal(st1, st0)
+                assert np.all(it1 <= it0)  # (warm-started at the step's solution: at most as many)
+            s.close()
+        finally:
+            os.environ.pop("MPCQ_KERNEL", None)
+    assert np.array_equal(res["tile"][0], res["wave"][0]) and np.array_equal(res["tile"][1], res["wave"][1])
+    assert np.abs(res["tile"][0] - q).max() <= 1e-12 * max(1.0, np.abs(q).max())
+    assert np.abs(res["tile"][1] - u).max() <= 1e-12 * max(1.0, np.abs(u).max())
+
+
 @pytest.mark.gpu
 def test_phase_chain_counters_across_solves(plant, monkeypatch):
     """One context, consecutive cold solves whose phase chains differ in length (default, one launch,
