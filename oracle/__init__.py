@@ -120,7 +120,7 @@ def lib() -> C.CDLL:
     L.ora_condense_mimo.argtypes = [C.POINTER(_MimoPlant), C.POINTER(_MimoOps)]
     L.ora_mimo_plants_step.restype = C.c_int
     L.ora_mimo_plants_step.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, dp, dp, dp, dp, dp, dp,
-                                       dp, dp, dp, dp, dp, dp, C.POINTER(Settings), dp, dp, ip, ip, C.c_int]
+                                       dp, dp, dp, dp, dp, dp, C.POINTER(Settings), dp, dp, ip, ip, C.c_int, dp]
     _LIB = L
     return L
 
@@ -229,9 +229,10 @@ def mimo_upper_bound(ops: dict, X, U) -> np.ndarray:
 
 
 def mimo_plants_step(shared: dict, Ad, Bd, X, U, N: int, yref=None, settings: Settings | None = None,
-                     nthreads: int = 0, s_rows: int | None = None):
+                     nthreads: int = 0, s_rows: int | None = None, margins: bool = False):
     """Per-plant MIMO batch (config 4): condense + setup + one controllerStep per plant.
-    Returns (U_new (k, nu), x (k, n), status, iters)."""
+    Returns (U_new (k, nu), x (k, n), status, iters) and, with ``margins``, each QP's decision
+    margin (Info.margin)."""
     Ad, Bd, X, U = _c64(Ad), _c64(Bd), _c64(X), _c64(U)
     k, nx, nu = Bd.shape
     ny = np.asarray(shared["Cd"]).shape[0]
@@ -243,10 +244,12 @@ def mimo_plants_step(shared: dict, Ad, Bd, X, U, N: int, yref=None, settings: Se
     x_out = np.zeros((k, n))
     st = np.zeros(k, dtype=np.int32)
     it = np.zeros(k, dtype=np.int32)
+    mg = np.zeros(k)
     lib().ora_mimo_plants_step(k, nx, nu, ny, N, N if s_rows is None else s_rows, _dp(Ad), _dp(Bd), _dp(sh["Cd"]),
                                _dp(sh["Q"]), _dp(sh["R"]), _dp(sh["RD"]), _dp(sh["K"]), _dp(sh["K0"]), _dp(sh["w0"]),
-                               _dp(X), _dp(U), _dp(yr), C.byref(s), _dp(U_out), _dp(x_out), _ip(st), _ip(it), nthreads)
-    return U_out, x_out, st, it
+                               _dp(X), _dp(U), _dp(yr), C.byref(s), _dp(U_out), _dp(x_out), _ip(st), _ip(it), nthreads,
+                               _dp(mg))
+    return (U_out, x_out, st, it, mg) if margins else (U_out, x_out, st, it)
 
 
 # ----------------------------------------------------------------------------- OSQP restatement

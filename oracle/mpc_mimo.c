@@ -186,7 +186,8 @@ int ora_mimo_plants_step(int n_plants, int nx, int nu, int ny, int N, int s_rows
                          const double *Bd, const double *Cd, const double *Q, const double *R,
                          const double *RD, const double *K, const double *K0, const double *w0,
                          const double *X, const double *U, const double *yref, const ora_settings *s,
-                         double *U_out, double *x_out, int *status, int *iters, int nthreads)
+                         double *U_out, double *x_out, int *status, int *iters, int nthreads,
+                         double *margin)
 {
     int failed = 0;
 #ifdef _OPENMP
@@ -236,6 +237,7 @@ int ora_mimo_plants_step(int n_plants, int nx, int nu, int ny, int N, int s_rows
             ora_get_info(w, &info);
             status[pp] = info.status;
             iters[pp] = info.iter;
+            if (margin) margin[pp] = info.margin;
             const double *x = ora_solution_x(w);
             if (x_out)
                 for (int i = 0; i < n; i++) x_out[(size_t)pp * n + i] = x[i];

@@ -58,12 +58,14 @@ void ora_mimo_upper_bound(const ora_mimo_plant *pl, const ora_mimo_ops *o, const
 /* Per-plant batch (BASELINE config 4): plant p has its own Ad[p], Bd[p]; Cd, Q, R, RD, K, K0, w0 are
  * shared.  For each plant: condense, osqp setup with the ctor's data (q0 = 0, l = -DBL_MAX, u0 = W0),
  * one controllerStep from (X[p], U[p]) (U[p] += x[0:nu] when solved).  OpenMP over plants.
+ * margin (nullable): each plant's decision margin (ora_info.margin).
  * Returns the number of plants whose setup failed. */
 int ora_mimo_plants_step(int n_plants, int nx, int nu, int ny, int N, int s_rows, const double *Ad,
                          const double *Bd, const double *Cd, const double *Q, const double *R,
                          const double *RD, const double *K, const double *K0, const double *w0,
                          const double *X, const double *U, const double *yref, const ora_settings *s,
-                         double *U_out, double *x_out, int *status, int *iters, int nthreads);
+                         double *U_out, double *x_out, int *status, int *iters, int nthreads,
+                         double *margin);
 
 #ifdef __cplusplus
 }

@@ -274,7 +274,8 @@ struct MimoSetupArgs {
     double sigma;
     const double *Ad, *Bd, *Cd, *Q, *R, *RD, *K, *K0, *w0;  // [plant] nx*nx, nx*nu, ny*nx, ny*ny, nu*nu x2, nu*nx, nu*nu, nu
     double *ops;                                            // [plant] MimoLayout::total
-    int *flags;                                             // OR: 1 setup failed, 2 a row is not an inequality,
+    int *flags;                                             // OR: 1 a diagonal of P^ + sigma I is not positive
+                                                            //     (non-convex), 2 a row is not an inequality,
                                                             //     4 some K0 is not diagonal
     long long *stamps;                                      // debug (MPCQ_MIMO_SETUP_STAMPS): 16 per plant, or null
 };

@@ -417,7 +417,12 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
     // ---- outputs: P^ = c D P D, D, E, c, SW (suffix sums of K0' diag(2 E_k^2) K0), row-type check
     for (int e = t; e < n * L.ldp; e += T) {
         const int i = e / L.ldp, j = e % L.ldp;
-        out[L.Ph + e] = j < n ? ((cst * Dv[i]) * P[(size_t)i * ldp + j]) * Dv[j] : 0.0;
+        const double v = j < n ? ((cst * Dv[i]) * P[(size_t)i * ldp + j]) * Dv[j] : 0.0;
+        out[L.Ph + e] = v;
+        // osqp_setup fails on a non-convex P (the reference's ctor: solverFlag false); a diagonal of
+        // P^ + sigma I that is not positive proves it.  (Necessary only: a P with positive diagonal
+        // that is still indefinite surfaces as the QP's NON_CVX status at the solve's factorisation.)
+        if (i == j && !(v + a.sigma > 0.0)) atomicOr(a.flags, 1);
     }
     for (int j = t; j < n; j += T) {
         out[L.D + j] = Dv[j];

@@ -4,10 +4,13 @@ condensing + OSQP-0.6 restatement), same plants and states.
 
 The reference is SISO only, so the MIMO formulation is pinned two ways: its SISO specialisation is
 bit-identical to the reference-pinned SISO condensing (test_oracle.py), and here the device path
-run at n_u = 1 reproduces the reference controller's controllerStep.  Bar (fp64 throughout): the
-oracle's status for every QP, its iteration count for >= 95% of QPs (the device inverts the reduced
-KKT matrix where the oracle factors the full KKT system, so a residual that sits on a termination
-threshold can flip), and on those |x - x_oracle| <= 1e-7 max(1, |x|), the applied U to 1e-7.
+run at n_u = 1 reproduces the reference controller's controllerStep.  Bar (fp64 throughout), on
+EVERY QP: the oracle's status, and its iteration count with |x - x_oracle| <= 1e-7 max(1, |x|) and
+the applied U to 1e-7.  Exception, counted and bounded: the device inverts the reduced KKT matrix
+where the oracle factors the full KKT system (rounding ~1e-12 relative), so a QP whose schedule
+decision the oracle itself takes within TIE_MARGIN of its threshold (|ln(residual / tolerance)|,
+oracle Info.margin) may take the other branch; such a QP must still carry the oracle's status
+(a SOLVED answer one check earlier or later, terminated by the device's own fp64 test).
 """
 import numpy as np
 import pytest
@@ -17,6 +20,7 @@ import solvempc_amd as sm
 from solvempc_amd import workload
 
 pytestmark = pytest.mark.gpu
+TIE_MARGIN = 1e-6
 
 
 def _dev(a):
@@ -49,10 +53,12 @@ def _run_device(shared, Ad, Bd, X, U, N, s_rows=None, yref=None, steps=1, settin
     return Us, s.solution(), st, it
 
 
-def _check(x, st, it, U1, x_ref, st_ref, it_ref, U_ref, tol=1e-7):
+def _check(x, st, it, U1, x_ref, st_ref, it_ref, U_ref, margin, tol=1e-7):
     assert np.array_equal(st, st_ref), (st, st_ref)
     same = it == it_ref
-    assert same.mean() >= 0.95, f"iteration schedule matches on {same.mean():.1%}: {it[~same]} vs {it_ref[~same]}"
+    assert np.all(same | (margin < TIE_MARGIN)), (np.flatnonzero(~same), it[~same], it_ref[~same], margin[~same])
+    if not same.all():
+        print(f"{int((~same).sum())} of {len(same)} QPs took a tie's other branch (margins {margin[~same]})")
     rel = np.abs(x[same] - x_ref[same]).max(axis=1) / np.maximum(1.0, np.abs(x_ref[same]).max(axis=1))
     assert rel.max() < tol, rel.max()
     assert np.abs(U1[same] - U_ref[same]).max() < tol
@@ -64,9 +70,9 @@ def test_quadrotor_step_matches_oracle():
     sh = workload.quadrotor_shared()
     X, U = workload.quadrotor_states(3, 0, B)
     Us, x, st, it = _run_device(sh, Ad, Bd, X, U, N)
-    U_ref, x_ref, st_ref, it_ref = oracle.mimo_plants_step(sh, Ad, Bd, X, U, N, nthreads=8)
+    U_ref, x_ref, st_ref, it_ref, mg = oracle.mimo_plants_step(sh, Ad, Bd, X, U, N, nthreads=8, margins=True)
     assert np.all(st == sm.SOLVED)
-    _check(x, st, it, Us[0], x_ref, st_ref, it_ref, U_ref)
+    _check(x, st, it, Us[0], x_ref, st_ref, it_ref, U_ref, mg)
 
 
 def test_siso_specialisation_matches_reference_controller(plant):
@@ -80,9 +86,9 @@ def test_siso_specialisation_matches_reference_controller(plant):
     X, U = workload.mpc_states(3, 0, B)
     Us, x, st, it = _run_device(sh, Ad, Bd, X, U[:, None], N, s_rows=10)
     U_ref, st_ref, it_ref = oracle.plants_step(plant, Ad, Bd[:, :, 0], X, U, N)
-    _, x_ref, st2, it2 = oracle.mimo_plants_step(sh, Ad, Bd, X, U[:, None], N, s_rows=10)
+    _, x_ref, st2, it2, mg = oracle.mimo_plants_step(sh, Ad, Bd, X, U[:, None], N, s_rows=10, margins=True)
     assert np.array_equal(st_ref, st2) and np.array_equal(it_ref, it2)  # the two oracles agree
-    _check(x, st, it, Us[0][:, 0], x_ref, st_ref, it_ref, U_ref)
+    _check(x, st, it, Us[0][:, 0], x_ref, st_ref, it_ref, U_ref, mg)
 
 
 def test_random_mimo_with_state_bounds_and_reference():
@@ -101,8 +107,8 @@ def test_random_mimo_with_state_bounds_and_reference():
     U = 0.2 * rng.normal(size=(B, nu))
     yref = np.array([0.3, -0.2])
     Us, x, st, it = _run_device(sh, Ad, Bd, X, U, N, s_rows=5, yref=yref)
-    U_ref, x_ref, st_ref, it_ref = oracle.mimo_plants_step(sh, Ad, Bd, X, U, N, yref=yref, s_rows=5)
-    _check(x, st, it, Us[0], x_ref, st_ref, it_ref, U_ref)
+    U_ref, x_ref, st_ref, it_ref, mg = oracle.mimo_plants_step(sh, Ad, Bd, X, U, N, yref=yref, s_rows=5, margins=True)
+    _check(x, st, it, Us[0], x_ref, st_ref, it_ref, U_ref, mg)
 
 
 def test_second_step_is_warm_started():
@@ -138,9 +144,10 @@ def test_settings_variants_match_oracle(over):
     sh = workload.quadrotor_shared()
     X, U = workload.quadrotor_states(7, 0, B)
     Us, x, st, it = _run_device(sh, Ad, Bd, X, U, N, settings=sm.default_settings(**over))
-    U_ref, x_ref, st_ref, it_ref = oracle.mimo_plants_step(sh, Ad, Bd, X, U, N, settings=oracle.default_settings(**over),
-                                                           nthreads=8)
-    _check(x, st, it, Us[0], x_ref, st_ref, it_ref, U_ref)
+    U_ref, x_ref, st_ref, it_ref, mg = oracle.mimo_plants_step(sh, Ad, Bd, X, U, N,
+                                                               settings=oracle.default_settings(**over),
+                                                               nthreads=8, margins=True)
+    _check(x, st, it, Us[0], x_ref, st_ref, it_ref, U_ref, mg)
 
 
 def test_general_k0_path_on_diagonal_k0(monkeypatch):
@@ -151,5 +158,18 @@ def test_general_k0_path_on_diagonal_k0(monkeypatch):
     sh = workload.quadrotor_shared()
     X, U = workload.quadrotor_states(9, 0, B)
     Us, x, st, it = _run_device(sh, Ad, Bd, X, U, N)
-    U_ref, x_ref, st_ref, it_ref = oracle.mimo_plants_step(sh, Ad, Bd, X, U, N, nthreads=8)
-    _check(x, st, it, Us[0], x_ref, st_ref, it_ref, U_ref)
+    U_ref, x_ref, st_ref, it_ref, mg = oracle.mimo_plants_step(sh, Ad, Bd, X, U, N, nthreads=8, margins=True)
+    _check(x, st, it, Us[0], x_ref, st_ref, it_ref, U_ref, mg)
+
+
+def test_nonconvex_plant_fails_setup():
+    """A plant whose condensed Hessian has a negative diagonal (R < 0 beyond the tracking term) is
+    rejected at setup, as osqp_setup rejects a non-convex P (the reference's ctor: solverFlag false),
+    instead of surfacing later as a per-QP NON_CVX status."""
+    N, B = 30, 4
+    Ad, Bd = workload.quadrotor_plants(3, 0, B)
+    sh = dict(workload.quadrotor_shared())
+    sh["R"] = -1e6 * np.eye(4)
+    X, U = workload.quadrotor_states(3, 0, B)
+    with pytest.raises(sm.MpcqError, match="not positive definite"):
+        _run_device(sh, Ad, Bd, X, U, N)
