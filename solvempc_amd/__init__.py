@@ -193,7 +193,9 @@ class BatchSolver:
 
     def mpc_run_device(self, X_ptr: int, U_ptr: int, xref: float, steps: int, seed: int, first_qp: int,
                        first_step: int, noise_std: float, stream: int) -> None:
-        """``steps`` warm-started [controllerStep; plant update] rounds, replayed from a hipGraph."""
+        """``steps`` warm-started [controllerStep; plant update] rounds: one persistent launch on the
+        one-QP-per-wave path (every wave runs its QP through all the steps), else replayed from a
+        hipGraph."""
         _capi.check(lib().mpcq_mpc_run_device(self._ctx, C.c_void_p(X_ptr), C.c_void_p(U_ptr), float(xref),
                                               int(steps), seed, first_qp, first_step, float(noise_std),
                                               C.c_void_p(stream)), "mpcq_mpc_run_device")

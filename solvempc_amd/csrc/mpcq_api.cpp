@@ -1056,6 +1056,24 @@ int mpcq_mpc_simulate_device(mpcq_ctx *c, double *X, const double *U, unsigned l
     return MPCQ_OK;
 }
 
+// The stream in one launch (stream_wave_kernel, mpcq_wave.h): the one-QP-per-wave path's control
+// steps with the plant update between them, no per-step launches or graph.
+}  // extern "C"
+template <typename T>
+static int launch_stream(mpcq_ctx *c, hipStream_t s, double *X, double *U, double xref, const mpcq::StreamArgs &sa)
+{
+    auto a = make_args<T>(c);
+    a.mpc = 1; a.mpc_u = 1; a.nx = c->nx; a.X = X; a.U = U; a.xref = xref;
+    a.Fx = c->d_Fx; a.Fu = c->d_Fu; a.Fr = c->d_Fr; a.Sbar = c->d_Sbar; a.Ku = c->d_Ku; a.W0 = c->d_W0;
+    a.q_out = c->d_q; a.u_out = c->d_u;
+    a.stop_iter = c->set.max_iter;
+    c->qu_lazy = false;
+    return std::is_same<T, float>::value
+               ? mpcq_internal_stream_launch_f32((const mpcq::AdmmArgs<float> *)&a, c->nc, c->mc, &sa, s)
+               : mpcq_internal_stream_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->nc, c->mc, &sa, s);
+}
+extern "C" {
+
 int mpcq_mpc_run_device(mpcq_ctx *c, double *X, double *U, double xref, int steps, unsigned long long seed,
                         long long first_qp, long long first_step, double noise_std, void *stream)
 {
@@ -1082,6 +1100,20 @@ int mpcq_mpc_run_device(mpcq_ctx *c, double *X, double *U, double xref, int step
         return e == hipSuccess ? MPCQ_OK : fail(MPCQ_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
     };
     if ((rc = stage("set_step"))) return rc;
+    // one-QP-per-wave batches (small shared-plant batches, per-plant batches): one persistent launch
+    // (MPCQ_STREAM=graph: the per-step hipGraph below, the A/B and test cross-check)
+    if (choose_path(c).kind == MPCQ_PATH_WAVE && c->dims.n <= 32 && c->dims.m <= 64 &&
+        std::strcmp(test_hook("MPCQ_STREAM"), "graph") != 0) {
+        const mpcq::StreamArgs sa{steps, c->nx, c->dims.n_plants == 1, c->d_Ad, c->d_Bd, seed, first_qp, first_step,
+                                  noise_std};
+        const int lrc = c->dims.dtype == MPCQ_F32 ? launch_stream<float>(c, s, X, U, xref, sa)
+                                                  : launch_stream<double>(c, s, X, U, xref, sa);
+        if (lrc) return fail(MPCQ_ERR_HIP, std::string("stream kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+        if (mpcq_internal_set_step(c->d_step, first_step + steps, s)) return fail(MPCQ_ERR_HIP, "set_step launch failed");
+        c->fresh = false;
+        c->last = s;
+        return stage("stream kernel");
+    }
     int done = 0;
     if (c->fresh) {  // a reset is a one-off (x = z = y = 0): run that step eagerly, capture the rest
         if ((rc = launch_solve(c, s, true, X, U, xref))) return rc;

@@ -269,6 +269,16 @@ struct MimoLayout {
     }
 };
 
+// Persistent receding-horizon stream (config 5): control steps first_step .. first_step + steps - 1 of
+// the simulated plant X <- Ad X + Bd U + w (mpcq_plant_sim.h) between the solves.
+struct StreamArgs {
+    int steps, nx, shared;        // shared: every QP's plant is plant 0
+    const double *Ad, *Bd;        // [plant] nx*nx, nx
+    unsigned long long seed;
+    long long first_qp, first_step;
+    double noise_std;
+};
+
 struct MimoSetupArgs {
     int n_plants, N, nx, nu, ny, s_rows, scaling;
     double sigma;
@@ -342,6 +352,12 @@ int mpcq_internal_tile_launch_f32(const mpcq::AdmmArgs<float> *a, int KN, int KM
 // -1 = n > 32 or m > 64 (not compiled).
 int mpcq_internal_wave_launch_f64(const mpcq::AdmmArgs<double> *a, int nc, int mc, int grid, hipStream_t s);
 int mpcq_internal_wave_launch_f32(const mpcq::AdmmArgs<float> *a, int nc, int mc, int grid, hipStream_t s);
+// The receding-horizon stream in one launch (mpcq_wave.h stream_wave_kernel): every wave owns one QP
+// for all `steps` control steps (solve, U += x0, plant update).  0 launched, -1 no compiled capacity.
+int mpcq_internal_stream_launch_f32(const mpcq::AdmmArgs<float> *a, int nc, int mc, const mpcq::StreamArgs *sa,
+                                    hipStream_t s);
+int mpcq_internal_stream_launch_f64(const mpcq::AdmmArgs<double> *a, int nc, int mc, const mpcq::StreamArgs *sa,
+                                    hipStream_t s);
 // Plant update of the receding-horizon stream (mpcq_stream.hip); step from *step_p when non-null.
 int mpcq_internal_simulate(int batch, int nx, int shared, const double *Ad, const double *Bd, double *X,
                            const double *U, unsigned long long seed, long long first_qp, const long long *step_p,

@@ -1,29 +1,10 @@
 // solvempc_amd/csrc/mpcq_stream.hip — the simulated plant of the receding-horizon stream
-// (BASELINE config 5): the reference's control loop (src/solver.cpp:43-74) reads the plant state
-// from a serial port; here every QP's plant evolves on the device between control steps,
-//     X <- Ad X + Bd U + w,   w ~ N(0, noise_std^2 I),
-// with w from a counter-based generator (SplitMix64 of (seed, global QP index, draw), Box-Muller),
-// restated in solvempc_amd/workload.py so tests can reproduce every draw on the host.
+// (BASELINE config 5), one launch per control step (the hipGraph path of mpcq_mpc_run_device and
+// mpcq_mpc_simulate_device); the row arithmetic and the noise are mpcq_plant_sim.h's.
 #include "mpcq_internal.h"
-
-#include <math.h>
+#include "mpcq_plant_sim.h"
 
 namespace mpcq {
-
-__device__ __forceinline__ unsigned long long splitmix64(unsigned long long z)
-{
-    z += 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-
-// uniform in (0, 1) for (seed, global index, draw) — workload.uniforms
-__device__ __forceinline__ double uni(unsigned long long key, unsigned long long idx, unsigned long long d)
-{
-    const unsigned long long x = splitmix64(key ^ (idx * 0x100000001B3ull + d * 0xD6E8FEB86659FD93ull));
-    return ((double)(x >> 11) + 0.5) * (1.0 / 9007199254740992.0);
-}
 
 // One thread per QP.  Plant arrays: Ad [plant][nx][nx], Bd [plant][nx] (plant 0 when shared).
 __global__ void simulate_kernel(int batch, int nx, int shared, const double *Ad, const double *Bd, double *X,
@@ -38,23 +19,9 @@ __global__ void simulate_kernel(int batch, int nx, int shared, const double *Ad,
     double x[8], xn[8];
     for (int t = 0; t < 8; t++) x[t] = t < nx ? X[(size_t)b * nx + t] : 0.0;
     const double u = U[b];
-    const unsigned long long key = splitmix64(seed * 0x632BE59BD9B4E019ull + 1ull);
+    const unsigned long long key = sim_key(seed);
     const unsigned long long idx = (unsigned long long)(first_qp + b);
-    const int np = (nx + 1) / 2;  // Box-Muller pairs: w[t] = r_t cos th_t (t < np), r_{t-np} sin th_{t-np}
-    for (int i = 0; i < nx; i++) {
-        double s = 0.0;
-        for (int t = 0; t < nx; t++) s += A[i * nx + t] * x[t];
-        s += B[i] * u;
-        double w = 0.0;
-        if (noise_std != 0.0) {
-            const int p = i < np ? i : i - np;
-            const unsigned long long d0 = (unsigned long long)step * 64ull + 2ull * p;
-            const double r = sqrt(-2.0 * log(uni(key, idx, d0)));
-            const double th = 2.0 * M_PI * uni(key, idx, d0 + 1);
-            w = noise_std * (i < np ? r * cos(th) : r * sin(th));
-        }
-        xn[i] = s + w;
-    }
+    for (int i = 0; i < nx; i++) xn[i] = sim_row(i, nx, A, B, x, u, key, idx, step, noise_std);
     for (int i = 0; i < nx; i++) X[(size_t)b * nx + i] = xn[i];
 }
 

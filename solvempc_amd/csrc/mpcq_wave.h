@@ -14,6 +14,7 @@
 // launch to a wave launch at a phase boundary: both run OSQP's iteration on the same state (x', z, y,
 // rho), with the products summed in different orders (last-bit differences, like any two OSQP builds).
 #pragma once
+#include "mpcq_plant_sim.h"
 #include "mpcq_tile.h"
 
 namespace mpcq {
@@ -84,7 +85,7 @@ template <typename T, int CAP>
 __device__ __forceinline__ T mem_dot(const T *M, size_t stride, const T *bc, T acc)
 {
     bc += opaque(0);
-#pragma unroll
+#pragma unroll 4
     for (int i = 0; i < CAP; i++) acc = tt_fma(M[(size_t)i * stride], bc[i], acc);
     return acc;
 }
@@ -137,7 +138,8 @@ __device__ __noinline__ void build_minv(const T *ops, const int *ctype, const Op
 }
 
 template <typename T, int NCAP, int MCAP, bool ALL_INEQ, bool LFREE>
-__device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int mc, int b, T *bcx, T *bcw, double *mi)
+__device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int mc, int b, T *bcx, T *bcw, double *mi,
+                                               bool fresh_ok = true)
 {
     constexpr int VEC = 16 / sizeof(T);
     constexpr int BN = (NCAP + VEC - 1) / VEC * VEC, BM = (MCAP + VEC - 1) / VEC * VEC;
@@ -241,12 +243,13 @@ __device__ __forceinline__ void wave_solve_one(const AdmmArgs<T> &a, int nc, int
     T xs = T(0), z = T(0), y = T(0), rho;
     int it = 0;
     const int ncs = nc, mcs = mc;
-    const bool load_state = a.resume || (a.warm && !a.fresh);
+    const bool fresh = a.fresh && fresh_ok;  // (the stream kernel: a reset applies to its first step only)
+    const bool load_state = a.resume || (a.warm && !fresh);
     if (a.resume) {
         rho = a.rhos[b];
         it = a.it_state[b];
     } else {
-        rho = a.fresh ? (T)fmin(fmax(st.rho, kRhoMin), kRhoMax) : a.rhos[b];
+        rho = fresh ? (T)fmin(fmax(st.rho, kRhoMin), kRhoMax) : a.rhos[b];
     }
     if (load_state) {
         if (ln) xs = a.xs[(size_t)b * ncs + lane];
@@ -571,6 +574,59 @@ __global__ __launch_bounds__(64, 2) void admm_wave_kernel(AdmmArgs<T> a, int nc,
 }
 
 
+// The receding-horizon stream (BASELINE config 5; the reference's loop solver.cpp:43-74 around
+// controllerStep :81-108) in ONE launch.  QPs of different plants never interact, so a wave owns its
+// QP for all sa.steps control steps: controllerStep (front end, warm-started solve, U += x0), then the
+// simulated plant X <- Ad X + Bd U + w (lane i: row i, mpcq_plant_sim.h), then the next step.  It
+// replaces a hipGraph of three launches per step, whose step lasted as long as the batch's slowest QP;
+// here a wave's run lasts its own QP's iterations summed over the steps.  Every operation is the
+// per-step path's (wave_solve_one, sim_row), so the trajectory is bit-identical to it.  The state
+// (x', z, y, rho, X, U) goes through HBM between steps as it does between launches; one wave writes
+// and reads it, ordered by workgroup-scope fences (the workgroup is this one wave).
+template <typename T, int NCAP, int MCAP, bool ALL_INEQ, bool LFREE>
+#ifndef MPCQ_STREAM_WPE
+#define MPCQ_STREAM_WPE 2
+#endif
+__global__ __launch_bounds__(64, MPCQ_STREAM_WPE) void stream_wave_kernel(AdmmArgs<T> a, int nc, int mc, StreamArgs sa)
+{
+    static_assert(NCAP <= 64 && MCAP <= 64, "one row per lane");
+    constexpr int VEC = 16 / sizeof(T);
+    constexpr int BN = (NCAP + VEC - 1) / VEC * VEC, BM = (MCAP + VEC - 1) / VEC * VEC;
+    __shared__ __attribute__((aligned(16))) T bcx[BN];
+    __shared__ __attribute__((aligned(16))) T bcw[BM];
+    __shared__ double mi[NCAP * (NCAP + 1)];
+    const int lane = threadIdx.x, nx = sa.nx;
+    const unsigned long long key = sim_key(sa.seed);
+    for (int slot = blockIdx.x; slot < a.batch; slot += gridDim.x) {  // uniform: one wave per block
+        const int b = a.qp0 + slot;
+        const double *Ad = sa.Ad + (sa.shared ? 0 : (size_t)b * nx * nx);
+        const double *Bd = sa.Bd + (sa.shared ? 0 : (size_t)b * nx);
+        for (int k = 0; k < sa.steps; k++) {
+            wave_solve_one<T, NCAP, MCAP, ALL_INEQ, LFREE>(a, nc, mc, b, bcx, bcw, mi, k == 0);
+            __threadfence_block();  // this step's U (lane 0) and state before the plant update reads them
+            double x[8];
+#pragma unroll
+            for (int t = 0; t < 8; t++) x[t] = t < nx ? a.X[(size_t)b * nx + t] : 0.0;
+            const double u = a.U[b];
+            const double xn = lane < nx ? sim_row(lane, nx, Ad, Bd, x, u, key, (unsigned long long)(sa.first_qp + b),
+                                                  sa.first_step + k, sa.noise_std)
+                                        : 0.0;
+            if (lane < nx) const_cast<double *>(a.X)[(size_t)b * nx + lane] = xn;
+            __threadfence_block();  // the next step's front end reads X
+        }
+    }
+}
+
+template <typename T, int NCAP, int MCAP>
+int stream_launch(const AdmmArgs<T> &a, int nc, int mc, const StreamArgs &sa, hipStream_t s)
+{
+    if (a.all_ineq && a.lower_free)
+        hipLaunchKernelGGL((stream_wave_kernel<T, NCAP, MCAP, true, true>), dim3(a.batch), dim3(64), 0, s, a, nc, mc, sa);
+    else
+        hipLaunchKernelGGL((stream_wave_kernel<T, NCAP, MCAP, false, false>), dim3(a.batch), dim3(64), 0, s, a, nc, mc, sa);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 template <typename T, int NCAP, int MCAP>
 int wave_launch(const AdmmArgs<T> &a, int nc, int mc, int grid, hipStream_t s)
 {
@@ -595,6 +651,22 @@ int wave_launch_any(const AdmmArgs<T> &a, int nc, int mc, int grid, hipStream_t 
     MPCQ_WAVE_CAPS(MPCQ_PICK)
 #undef MPCQ_PICK
 #define MPCQ_TRY(NC_, MC_) if (bn == NC_ && bm == MC_) return wave_launch<T, NC_, MC_>(a, nc, mc, grid, s);
+    MPCQ_WAVE_CAPS(MPCQ_TRY)
+#undef MPCQ_TRY
+    return -1;
+}
+
+template <typename T>
+int stream_launch_any(const AdmmArgs<T> &a, int nc, int mc, const StreamArgs &sa, hipStream_t s)
+{
+    int best = -1, bn = 0, bm = 0;
+#define MPCQ_PICK(NC_, MC_)                                                  \
+    if (a.n <= NC_ && a.m <= MC_ && (best < 0 || NC_ * (NC_ + MC_) < best)) { \
+        best = NC_ * (NC_ + MC_); bn = NC_; bm = MC_;                         \
+    }
+    MPCQ_WAVE_CAPS(MPCQ_PICK)
+#undef MPCQ_PICK
+#define MPCQ_TRY(NC_, MC_) if (bn == NC_ && bm == MC_) return stream_launch<T, NC_, MC_>(a, nc, mc, sa, s);
     MPCQ_WAVE_CAPS(MPCQ_TRY)
 #undef MPCQ_TRY
     return -1;

@@ -5,3 +5,9 @@ extern "C" int mpcq_internal_wave_launch_f32(const mpcq::AdmmArgs<float> *a, int
 {
     return mpcq::wave_launch_any<float>(*a, nc, mc, grid, s);
 }
+
+extern "C" int mpcq_internal_stream_launch_f32(const mpcq::AdmmArgs<float> *a, int nc, int mc, const mpcq::StreamArgs *sa,
+                                              hipStream_t s)
+{
+    return mpcq::stream_launch_any<float>(*a, nc, mc, *sa, s);
+}

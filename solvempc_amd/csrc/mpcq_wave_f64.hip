@@ -5,3 +5,9 @@ extern "C" int mpcq_internal_wave_launch_f64(const mpcq::AdmmArgs<double> *a, in
 {
     return mpcq::wave_launch_any<double>(*a, nc, mc, grid, s);
 }
+
+extern "C" int mpcq_internal_stream_launch_f64(const mpcq::AdmmArgs<double> *a, int nc, int mc, const mpcq::StreamArgs *sa,
+                                              hipStream_t s)
+{
+    return mpcq::stream_launch_any<double>(*a, nc, mc, *sa, s);
+}

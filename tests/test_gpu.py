@@ -484,6 +484,46 @@ def test_receding_horizon_stream_f32(plant, kernel):
     assert len(tied) <= 2, tied
 
 
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_stream_one_launch_matches_graph(plant, dtype, monkeypatch):
+    """mpcq_mpc_run_device's one-launch stream (stream_wave_kernel: each wave runs its QP through all the
+    control steps) against the per-step hipGraph path (MPCQ_STREAM=graph) from the same cold state:
+    bit-identical X, U, statuses, iterations, rho and stream counters after 30 steps in one call,
+    then 7 more steps in a second call (warm state carried across calls), on a ragged batch."""
+    import torch
+    N, B = 20, 333
+    ops = oracle.condense(plant, N)
+    l = np.full(2 * N, LMIN)
+    u0 = oracle.upper_bound(ops, np.zeros(4), 0.0)
+    X, U = workload.stream_states(4, 0, B)
+
+    def run(mode):
+        if mode:
+            monkeypatch.setenv("MPCQ_STREAM", mode)
+        else:
+            monkeypatch.delenv("MPCQ_STREAM", raising=False)
+        s = sm.BatchSolver(N, 2 * N, B, dtype=dtype)
+        s.setup(ops["P"], np.zeros(N), ops["A"], l, u0)
+        s.mpc_set_operators(ops["Fx"], ops["Fu"], ops["Fr"], ops["Sbar"], ops["Ku"], ops["W0"])
+        s.mpc_set_plant(plant["Ad"], plant["Bd"])
+        Xd, Ud = torch.from_numpy(X.copy()).cuda(), torch.from_numpy(U.copy()).cuda()
+        st = torch.cuda.Stream()
+        out = []
+        for first, steps in ((0, 30), (30, 7)):
+            with torch.cuda.stream(st):
+                s.mpc_run_device(Xd.data_ptr(), Ud.data_ptr(), 0.0, steps, 4, 0, first, 1e-2, st.cuda_stream)
+            st.synchronize()
+            it_acc, uns = s.stream_counters()
+            out.append((Xd.cpu().numpy().copy(), Ud.cpu().numpy().copy(), *s.info(), it_acc, uns))
+        return out
+
+    graph, one = run("graph"), run(None)
+    for g, o in zip(graph, one):
+        for a, b in zip(g, o):
+            assert np.array_equal(a, b)
+    assert np.all(one[-1][2] == sm.SOLVED) and one[-1][6].sum() == 0  # (X, U, status, iter, rho, it_acc, uns)
+
+
 def test_stream_workload_stays_solved_and_bounded(plant):
     """The config-5 workload (workload.stream_states, noise std 1e-2) over 400 fp32 control steps: every
     plant SOLVED at every step and the closed loop bounded (the reference controller on its plant)."""
