@@ -486,7 +486,7 @@ def main_lti(a, rank, world, local, dist, dev):
                "batch_per_gpu": B, "horizon": N, "parallelism": f"dp{world}"} if perplant else
               {"workload": f"cfg5: {B} plants per GPU x {a.ctrl_steps} warm-started control steps, simulated plant "
                            f"(noise std {a.noise}, X0 ~ N(0, {workload.STREAM_X_SCALE}^2 diag(.1,.1,.05,.5)), U0 = 0), "
-                           f"{'one persistent launch' if solver.path()[0] == 'wave' else 'hipGraph-replayed'}, N={N}",
+                           f"one launch for all steps (tile stream mode where the shape allows), N={N}",
                "batch_per_gpu": B, "horizon": N, "ctrl_steps": a.ctrl_steps, "parallelism": f"dp{world}"})
     rec = _header(a, world, total_qps, wall, a.dtype, "QP solves/sec (n_x=4, n_u=1, N=20 batch)",
                   "synthetic (counter-based X ~ N(0, diag(.1,.1,.05,.5)), U ~ U(-1,1); reference plant config)"
@@ -496,8 +496,11 @@ def main_lti(a, rank, world, local, dist, dev):
         "bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS[a.dtype], "unit": "TFLOP/s",
         "frac": achieved / PEAK_TFLOPS[a.dtype], "traffic": traffic_per_solve(a.dtype, B, N) if not stream_mode else None,
         "mfma_util": mfma_util(a.dtype) if a.workload == "cfg2" and B == 65536 else None,
-        "kernel": ("stream_wave_kernel (one launch: every control step and plant update)"
-                   if stream_mode and kind == "wave" else
+        "kernel": ({"tile": "admm_tile_kernel, stream mode (one launch: every plant's control steps and "
+                            "plant updates, one plant per MFMA column)",
+                    "wave": "stream_wave_kernel (one launch: every control step and plant update)",
+                    "graph": f"admm_{kind}_kernel (per-step launches, hipGraph)"}[solver.stream_path()]
+                   if stream_mode else
                    f"admm_{kind}_kernel{' (paired loop)' if paired else ''} (all launches of "
                    f"{'the step' if not stream_mode else 'the control steps'})"),
         "kernel_ms": kern_ms, "flops_per_step": flops,

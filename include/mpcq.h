@@ -127,7 +127,7 @@ int mpcq_get_info(mpcq_ctx *ctx, int *status, int *iter, double *rho); /* each b
 int mpcq_get_scaling(mpcq_ctx *ctx, double *D, double *E, double *c); /* plant 0: n, m, 1 */
 
 /* Device path the next solve takes (no OSQP counterpart; for benchmarks and tests):
- * *kind = MPCQ_PATH_TILE (shared plant, MFMA tile kernel + one-QP-per-wave tail), MPCQ_PATH_WAVE
+ * *kind = MPCQ_PATH_TILE (shared plant, MFMA tile kernel's phase chain), MPCQ_PATH_WAVE
  * (one QP per wave: per-plant contexts, and shared-plant batches under 8,192 QPs) or MPCQ_PATH_LANE
  * (one QP per lane); *paired = 1 when the tile kernel runs its paired loop (rows n + j of A are the
  * negated rows j: the condensed-MPC constraint matrix). */
@@ -166,12 +166,20 @@ int mpcq_mpc_set_plant(mpcq_ctx *ctx, int nx, const double *Ad, const double *Bd
 /* One plant update on device-resident X (batch*nx) / U (batch); `step` selects the noise draw. */
 int mpcq_mpc_simulate_device(mpcq_ctx *ctx, double *X_dev, const double *U_dev, unsigned long long seed,
                              long long first_qp, long long step, double noise_std, void *stream);
-/* `steps` warm-started control steps  [controllerStep (:81-108) ; plant update]  for every QP,
- * captured once as a hipGraph and replayed (steps first_step .. first_step+steps-1).  X_dev/U_dev
- * evolve in place.  `stream` must not be the NULL stream (graph capture). */
+/* `steps` warm-started control steps  [controllerStep (:81-108) ; plant update]  for every QP
+ * (steps first_step .. first_step+steps-1); X_dev/U_dev evolve in place.  One launch runs every
+ * step: the tile kernel's stream mode for a shared plant of the condensed-MPC shape (each MFMA
+ * column one plant), else one QP per wave; other shapes replay a hipGraph of per-step launches.
+ * `stream` must not be the NULL stream (graph capture). */
 int mpcq_mpc_run_device(mpcq_ctx *ctx, double *X_dev, double *U_dev, double xref, int steps,
                         unsigned long long seed, long long first_qp, long long first_step,
                         double noise_std, void *stream);
+/* How the last mpcq_mpc_run_device call ran (benchmarks and tests): MPCQ_STREAM_TILE (one tile-kernel
+ * launch), MPCQ_STREAM_WAVE (one one-QP-per-wave launch) or MPCQ_STREAM_GRAPH (per-step launches). */
+#define MPCQ_STREAM_GRAPH 0
+#define MPCQ_STREAM_WAVE 1
+#define MPCQ_STREAM_TILE 2
+int mpcq_get_stream_path(mpcq_ctx *ctx, int *kind);
 /* Per-QP counters of the last mpcq_mpc_run_device call (host arrays of `batch` ints, synchronises):
  * the ADMM iterations of all its control steps, and the steps whose solve did not end SOLVED
  * (controllerStep returning false, :102, where the reference's loop would exit, solver.cpp:50). */

@@ -155,6 +155,12 @@ class BatchSolver:
         _capi.check(lib().mpcq_get_path(self._ctx, C.byref(k), C.byref(p)), "mpcq_get_path")
         return ("tile", "wave", "lane")[k.value], bool(p.value)
 
+    def stream_path(self) -> str:
+        """How the last mpc_run_device call ran: "tile" / "wave" (one launch) or "graph" (per-step)."""
+        k = C.c_int()
+        _capi.check(lib().mpcq_get_stream_path(self._ctx, C.byref(k)), "mpcq_get_stream_path")
+        return ("graph", "wave", "tile")[k.value]
+
     def device_view(self) -> dict:
         v = _capi.DeviceView()
         _capi.check(lib().mpcq_device_view_get(self._ctx, C.byref(v)), "mpcq_device_view_get")

@@ -128,6 +128,7 @@ struct mpcq_ctx {
     // receding-horizon stream counters (mpcq_mpc_run_device): per-QP iterations and unsolved steps
     int *d_it_acc = nullptr, *d_uns_acc = nullptr;
     bool stream_acc = false;  // launches made inside mpcq_mpc_run_device accumulate into them
+    int stream_path = MPCQ_STREAM_GRAPH;  // how the last mpcq_mpc_run_device call ran
     // host copies of plant-0 scaling
     std::vector<double> hD, hE;
     double hc = 1.0;
@@ -911,6 +912,13 @@ int mpcq_get_scaling(mpcq_ctx *c, double *D, double *E, double *cc)
     return MPCQ_OK;
 }
 
+int mpcq_get_stream_path(mpcq_ctx *c, int *kind)
+{
+    if (!c || !kind) return fail(MPCQ_ERR_ARG, "null argument");
+    *kind = c->stream_path;
+    return MPCQ_OK;
+}
+
 int mpcq_get_path(mpcq_ctx *c, int *kind, int *paired)
 {
     if (!c) return fail(MPCQ_ERR_ARG, "null context");
@@ -1074,6 +1082,42 @@ static int launch_stream(mpcq_ctx *c, hipStream_t s, double *X, double *U, doubl
 }
 extern "C" {
 
+// The stream in one tile launch (admm_tile_kernel STREAM mode): every MFMA column is one plant that runs
+// all its control steps, a wave holding `cpw` plants.  A control step of a column never waits for the
+// others', so a wave lives as long as its slowest plant's iterations summed over the steps (not the
+// per-step maximum over the batch); with a few thousand plants the chip is latency-bound, so cpw is
+// chosen to spread the plants over every SIMD (MPCQ_STREAM_CPW: A/B).  Needs adapt_rho and max_iter
+// on check iterations (multiples of check_termination, as OSQP's defaults are).
+}  // extern "C"
+template <typename T>
+static int launch_tile_stream(mpcq_ctx *c, hipStream_t s, double *X, double *U, double xref, mpcq::StreamArgs sa)
+{
+    const mpcq_settings &st = c->set;
+    const int ct = st.check_termination;
+    auto a = make_args<T>(c);
+    if (ct <= 0 || st.max_iter % ct || (st.adaptive_rho && a.adaptive_interval % ct)) return -1;
+    const char *e = test_hook("MPCQ_STREAM_CPW");
+    const long simds = (long)c->cus * 4;
+    sa.cpw = *e ? std::max(1, std::min(16, std::atoi(e)))
+                : (int)std::max<long>(1, std::min<long>(16, ((long)c->dims.batch + simds - 1) / simds));
+    a.mpc = 1; a.mpc_u = 1; a.nx = c->nx; a.X = X; a.U = U; a.xref = xref;
+    a.Fx = c->d_Fx; a.Fu = c->d_Fu; a.Fr = c->d_Fr; a.Sbar = c->d_Sbar; a.Ku = c->d_Ku; a.W0 = c->d_W0;
+    a.X_save = c->d_Xs; a.U_save = c->d_Us;  // the last step's X, U: its q, u on demand (materialize_qu)
+    a.paired = 1;
+    a.img = (const T *)c->d_img;
+    a.stop_iter = INT_MAX;
+    a.sim = sa;
+    const int rc = std::is_same<T, float>::value
+                       ? mpcq_internal_tile_stream_launch_f32((const mpcq::AdmmArgs<float> *)&a, c->KN, c->KM, s)
+                       : mpcq_internal_tile_stream_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->KN, c->KM, s);
+    if (rc == 0) {
+        c->qu_lazy = true;
+        c->lazy_xref = xref;
+    }
+    return rc;
+}
+extern "C" {
+
 int mpcq_mpc_run_device(mpcq_ctx *c, double *X, double *U, double xref, int steps, unsigned long long seed,
                         long long first_qp, long long first_step, double noise_std, void *stream)
 {
@@ -1100,11 +1144,30 @@ int mpcq_mpc_run_device(mpcq_ctx *c, double *X, double *U, double xref, int step
         return e == hipSuccess ? MPCQ_OK : fail(MPCQ_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
     };
     if ((rc = stage("set_step"))) return rc;
-    // one-QP-per-wave batches (small shared-plant batches, per-plant batches): one persistent launch
-    // (MPCQ_STREAM=graph: the per-step hipGraph below, the A/B and test cross-check)
+    // one launch for the whole stream: the tile kernel's stream mode for a shared plant of the paired
+    // condensed-MPC shape, else one QP per wave (per-plant batches); MPCQ_STREAM=graph: the per-step
+    // hipGraph below, MPCQ_STREAM=wave: the one-QP-per-wave launch (A/B and test cross-checks)
+    const char *smode = test_hook("MPCQ_STREAM");
+    const bool tile_ok = c->tile && c->paired && c->all_ineq && c->lower_free && c->d_Xs && c->d_Us &&
+                         std::strcmp(smode, "graph") != 0 && std::strcmp(smode, "wave") != 0 &&
+                         std::strcmp(test_hook("MPCQ_KERNEL"), "wave") != 0 && std::strcmp(test_hook("MPCQ_KERNEL"), "lane") != 0;
+    if (tile_ok) {
+        const mpcq::StreamArgs sa{steps, c->nx, c->dims.n_plants == 1, 0, c->d_Ad, c->d_Bd, seed, first_qp, first_step,
+                                  noise_std};
+        const int lrc = c->dims.dtype == MPCQ_F32 ? launch_tile_stream<float>(c, s, X, U, xref, sa)
+                                                  : launch_tile_stream<double>(c, s, X, U, xref, sa);
+        if (lrc == -2) return fail(MPCQ_ERR_HIP, std::string("tile stream launch failed: ") + hipGetErrorString(hipGetLastError()));
+        if (lrc == 0) {
+            if (mpcq_internal_set_step(c->d_step, first_step + steps, s)) return fail(MPCQ_ERR_HIP, "set_step launch failed");
+            c->fresh = false;
+            c->last = s;
+            c->stream_path = MPCQ_STREAM_TILE;
+            return stage("tile stream kernel");
+        }
+    }
     if (choose_path(c).kind == MPCQ_PATH_WAVE && c->dims.n <= 32 && c->dims.m <= 64 &&
-        std::strcmp(test_hook("MPCQ_STREAM"), "graph") != 0) {
-        const mpcq::StreamArgs sa{steps, c->nx, c->dims.n_plants == 1, c->d_Ad, c->d_Bd, seed, first_qp, first_step,
+        std::strcmp(smode, "graph") != 0) {
+        const mpcq::StreamArgs sa{steps, c->nx, c->dims.n_plants == 1, 1, c->d_Ad, c->d_Bd, seed, first_qp, first_step,
                                   noise_std};
         const int lrc = c->dims.dtype == MPCQ_F32 ? launch_stream<float>(c, s, X, U, xref, sa)
                                                   : launch_stream<double>(c, s, X, U, xref, sa);
@@ -1112,9 +1175,11 @@ int mpcq_mpc_run_device(mpcq_ctx *c, double *X, double *U, double xref, int step
         if (mpcq_internal_set_step(c->d_step, first_step + steps, s)) return fail(MPCQ_ERR_HIP, "set_step launch failed");
         c->fresh = false;
         c->last = s;
+        c->stream_path = MPCQ_STREAM_WAVE;
         return stage("stream kernel");
     }
     int done = 0;
+    c->stream_path = MPCQ_STREAM_GRAPH;
     if (c->fresh) {  // a reset is a one-off (x = z = y = 0): run that step eagerly, capture the rest
         if ((rc = launch_solve(c, s, true, X, U, xref))) return rc;
         if (mpcq_internal_simulate(c->dims.batch, c->nx, c->dims.n_plants == 1, c->d_Ad, c->d_Bd, X, U, seed,

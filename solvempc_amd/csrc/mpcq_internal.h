@@ -134,6 +134,17 @@ struct ListSeg {
 };
 
 // Arguments of the ADMM kernel (one QP per lane).
+// Persistent receding-horizon stream (config 5): control steps first_step .. first_step + steps - 1 of
+// the simulated plant X <- Ad X + Bd U + w (mpcq_plant_sim.h) between the solves.
+struct StreamArgs {
+    int steps, nx, shared;        // shared: every QP's plant is plant 0
+    int cpw;                      // tile stream: plants (columns) per wave
+    const double *Ad, *Bd;        // [plant] nx*nx, nx
+    unsigned long long seed;
+    long long first_qp, first_step;
+    double noise_std;
+};
+
 template <typename T>
 struct AdmmArgs {
     int batch, n, m;
@@ -182,6 +193,7 @@ struct AdmmArgs {
     int stop_iter;              // phase boundary (multiple of check_termination, or max_iter)
     int resume;                 // 1: phase >= 2 (state, rho and iteration count come from the buffers)
     long long *stamps;          // debug build (MPCQ_DEBUG_HOOKS): [wave][8] s_memtime stamps, or null
+    StreamArgs sim;             // the tile kernel's stream mode (tile_stream_launch): plants and noise
     // OSQP is_dual_infeasible needs ||P^ dx|| < c eps ||dx|| (norms as the termination mode reads them);
     // with lambda_min(P^) >= mu > 0 the left side is >= kappa ||dx|| (kappa from mu, D and n: host,
     // setup_on_device), so for kappa > 2 c eps the certificate cannot hold and its products are skipped
@@ -269,16 +281,6 @@ struct MimoLayout {
     }
 };
 
-// Persistent receding-horizon stream (config 5): control steps first_step .. first_step + steps - 1 of
-// the simulated plant X <- Ad X + Bd U + w (mpcq_plant_sim.h) between the solves.
-struct StreamArgs {
-    int steps, nx, shared;        // shared: every QP's plant is plant 0
-    const double *Ad, *Bd;        // [plant] nx*nx, nx
-    unsigned long long seed;
-    long long first_qp, first_step;
-    double noise_std;
-};
-
 struct MimoSetupArgs {
     int n_plants, N, nx, nu, ny, s_rows, scaling;
     double sigma;
@@ -348,6 +350,10 @@ int mpcq_internal_warm_f32(const mpcq::AdmmArgs<float> *a, int nc, int mc, const
 int mpcq_internal_tile_supported(int KN, int KM);
 int mpcq_internal_tile_launch_f64(const mpcq::AdmmArgs<double> *a, int KN, int KM, hipStream_t s);
 int mpcq_internal_tile_launch_f32(const mpcq::AdmmArgs<float> *a, int KN, int KM, hipStream_t s);
+// The receding-horizon stream in one tile launch (AdmmArgs::sim; every column one plant through all its
+// control steps).  0 launched, -1 not the paired condensed-MPC shape.
+int mpcq_internal_tile_stream_launch_f64(const mpcq::AdmmArgs<double> *a, int KN, int KM, hipStream_t s);
+int mpcq_internal_tile_stream_launch_f32(const mpcq::AdmmArgs<float> *a, int KN, int KM, hipStream_t s);
 // One-QP-per-wave path (mpcq_wave.h): grid blocks of 64 threads stride over the (listed) QPs;
 // -1 = n > 32 or m > 64 (not compiled).
 int mpcq_internal_wave_launch_f64(const mpcq::AdmmArgs<double> *a, int nc, int mc, int grid, hipStream_t s);

@@ -22,6 +22,7 @@
 // columns for long.  A QP's arithmetic does not depend on which wave or phase runs it.
 #pragma once
 #include "mpcq_internal.h"
+#include "mpcq_plant_sim.h"
 
 #include <cstdlib>
 #include <type_traits>
@@ -356,7 +357,8 @@ __device__ __forceinline__ void reg_mv(const T (&m1)[NTO][KS], const T (&x1)[G][
 #define MPCQ_TSTAMP(k, v) do { } while (0)
 #endif
 // WPB: waves per workgroup (4, or 8 so that an image set serves 8 waves and 4 waves/SIMD fit the LDS).
-template <typename T, int KN, int KM, bool ALL_INEQ, bool LFREE, int G, int OCC, bool PAIRED = false, int WPB = 4>
+template <typename T, int KN, int KM, bool ALL_INEQ, bool LFREE, int G, int OCC, bool PAIRED = false, int WPB = 4,
+          bool STREAM = false>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void admm_tile_kernel(AdmmArgs<T> a)
 {
     MPCQ_TSTAMP(0, (long long)__builtin_amdgcn_s_memtime());
@@ -378,6 +380,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     T *const s_E = rowv + 3 * NCP, *const s_Einv = rowv + 3 * NCP + MCP;
     // resumed phase: this workgroup serves list segment `seg` (ListSeg), as its workgroup `blk`
     const bool seglist = a.list_in != nullptr;
+    // receding-horizon stream (STREAM, AdmmArgs::sim): every column is one plant that runs all its
+    // control steps in this launch; a wave holds a.sim.cpw columns (the rest idle), QPs cpw w ..
+    constexpr bool refill = STREAM && G == 1;
     const int seg = blockIdx.x % ListSeg::kShards;
     const int count = seglist ? a.count_in[seg * ListSeg::kStride] : a.batch;  // slots of the list it serves
     const int blk = seglist ? (int)blockIdx.x / ListSeg::kShards : (int)blockIdx.x;
@@ -385,7 +390,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
         if (a.zero_cnt) a.zero_cnt[threadIdx.x * ListSeg::kStride] = 0;
         if (a.zero_cnt0) a.zero_cnt0[threadIdx.x * ListSeg::kStride] = 0;
     }
-    if (blk * QPW >= count) return;  // whole workgroup idle in this phase (uniform)
+    if (blk * (refill ? WPB * a.sim.cpw : QPW) >= count) return;  // whole workgroup idle in this phase (uniform)
     for (int i = threadIdx.x; i < NCP; i += NTH) {
         s_lam[i] = a.ops.lam[i];
         s_D[i] = a.ops.D[i];
@@ -481,10 +486,17 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
 
     // One group of 16 G QPs (column c of group gi: QP b_[gi], live if valid[gi]) through this
     // launch's phase.
-    auto run_group = [&](const int (&b_)[G], const bool (&valid)[G]) {
+    auto run_group = [&](const int (&b0_)[G], const bool (&valid0)[G]) {
     // lane indices re-derived opaquely, so that no lane-dependent address of the body is hoisted
     // and held live (in VGPRs) across the hot loop
     const int lane = opaque((int)threadIdx.x & 63), c = lane & 15, g = lane >> 4;
+    int b_[G];        // this lane's QP column (the refill schedule replaces finished ones)
+    bool valid[G];
+#pragma unroll
+    for (int gi = 0; gi < G; gi++) {
+        b_[gi] = b0_[gi];
+        valid[gi] = valid0[gi];
+    }
     const bool resume = a.resume != 0;
     const bool mpc_fe = a.mpc != 0;  // front end: the QP's first phase
 
@@ -496,13 +508,17 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     T xs[G][NS], z[G][MS], y[G][MS];     // state: x' (W-basis), z, y
     T rho[G], rinv[G];
     int it = 0;
-    {
-    // ---- per-QP data (element v = 4 s + g of this lane's QP column), per group.  Every global load
-    // of a group is issued (index clamped into the row, not branched) before any of it is used.
-    T qh[G][NS];  // q^ = c D q (osqp_update_lin_cost): prologue only; the checks re-read q (load_qh)
+    int cst[G];  // the wave iteration the column's QP started at (its own iteration: it - cst)
+    // ---- per-QP data of the columns in `fill` (element v = 4 s + g of this lane's QP column), per
+    // group: every column at entry, the refilled ones at a check (the others keep their registers and
+    // reproduce their W' q^ bit for bit).  Every global load of a group is issued (index clamped into
+    // the row, not branched) before any of it is used.
+    auto load_cols = [&](const bool (&fill)[G], const bool entry) {
+    T qh[G][NS];  // q^ = c D q (osqp_update_lin_cost); kept per wave in LDS (s_qh) for the checks
 #pragma unroll
     for (int gi = 0; gi < G; gi++) {
         const int b = b_[gi];
+        const bool pub = valid[gi] && fill[gi];  // this column's QP is (re)loaded: publish its outputs
         double qk[KN], up[KM], lo[LFREE ? 1 : KM];
         if (fe_on) {  // setF (:372-375) q = Fx X + Fu U + Fr ref;  (:93-99) u = W0 + Sbar X + Ku U
             // (a resumed phase recomputes them: X is read-only and U changes only at a QP's finalize)
@@ -523,9 +539,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                     if (t < nx) s0 += fe[FE_FX + 8 * v + t] * Xv[t];
                 const double s1 = fe[FE_FU + v] * Uv;
                 qk[s] = s0 + s1 + fe[FE_FR + v];
-                if (mpc_fe && a.q_out && valid[gi] && v < n) a.q_out[(size_t)b * n + v] = qk[s];
+                if (mpc_fe && a.q_out && pub && v < n) a.q_out[(size_t)b * n + v] = qk[s];
             }
-            if (mpc_fe && a.X_save && valid[gi]) {  // the step's X, U: q, u on demand (materialize_qu)
+            if (mpc_fe && a.X_save && pub) {  // the step's X, U: q, u on demand (materialize_qu)
                 if (g < nx) a.X_save[(size_t)b * nx + g] = a.X[(size_t)b * nx + g];  // (cache-hot reloads:
                 if (g + 4 < nx) a.X_save[(size_t)b * nx + g + 4] = a.X[(size_t)b * nx + g + 4];  // no register index by lane)
                 if (g == 0) a.U_save[b] = Uv;
@@ -539,7 +555,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 for (int t = 0; t < 8; t++)
                     if (t < nx) sx += fe[FE_SB + 8 * v + t] * Xv[t];
                 up[s] = fe[FE_W0 + v] + sx + fe[FE_KU + v] * Uv;
-                if (mpc_fe && a.u_out && valid[gi] && v < m) a.u_out[(size_t)b * m + v] = up[s];
+                if (mpc_fe && a.u_out && pub && v < m) a.u_out[(size_t)b * m + v] = up[s];
             }
             MPCQ_PRO_MARK(12);
         } else {
@@ -564,8 +580,14 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
 #pragma unroll
         for (int s = 0; s < NS; s++) {
             const int v = 4 * s + g;
-            qh[gi][s] = (s < KN && v < n) ? (T)((qk[s < KN ? s : 0] * fe[FE_D + v]) * c64) : T(0);
-            if (s < KN) s_qh[threadIdx.x >> 6][gi * KN + (s < KN ? s : 0)][lane] = qh[gi][s];
+            const int sk = s < KN ? s : 0;
+            const T qn = (s < KN && v < n) ? (T)((qk[sk] * fe[FE_D + v]) * c64) : T(0);
+            if (fill[gi]) {
+                qh[gi][s] = qn;
+                if (s < KN) s_qh[threadIdx.x >> 6][gi * KN + sk][lane] = qn;
+            } else {
+                qh[gi][s] = s < KN ? s_qh[threadIdx.x >> 6][gi * KN + sk][lane] : T(0);
+            }
         }
         MPCQ_PRO_MARK(13);
         int bad = 0, tchg = 0;
@@ -588,13 +610,15 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                     }
                 }
             }
-            uh[gi][s] = (T)uu;
-            if (!LFREE) lh[gi][s] = (T)ll;
-            if (!ALL_INEQ && gi == 0) rs[s] = (s < KM && v < m) ? (ctype[v] == -1 ? T(-1) : op.rscale[v]) : T(1);
+            if (fill[gi]) {
+                uh[gi][s] = (T)uu;
+                if (!LFREE) lh[gi][s] = (T)ll;
+            }
+            if (!ALL_INEQ && gi == 0 && entry) rs[s] = (s < KM && v < m) ? (ctype[v] == -1 ? T(-1) : op.rscale[v]) : T(1);
         }
         bad = col_or(bad);
         tchg = col_or(tchg);
-        status[gi] = bad ? kInvalidBounds : (tchg ? kTypeChanged : kUnsolved);
+        if (fill[gi]) status[gi] = bad ? kInvalidBounds : (tchg ? kTypeChanged : kUnsolved);
     }
     MPCQ_PRO_MARK(1);
     MPCQ_PRO_MARK(14);
@@ -608,15 +632,17 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     MPCQ_PRO_MARK(2);
 
     // ---- state: x' (W-basis), z, y; rho persists across solves (OSQP)
-    const bool load_state = resume || (a.warm && !a.fresh);
+    const bool fresh = a.fresh && entry;  // (a stream's reset applies to its first step only)
+    const bool load_state = resume || (a.warm && !fresh);
 #pragma unroll
     for (int gi = 0; gi < G; gi++) {
+        if (!fill[gi]) continue;
         const int b = b_[gi];
         if (resume) {
             rho[gi] = a.rhos[b];
             if (gi == 0) it = a.it_state[b];
         } else {
-            rho[gi] = a.fresh ? (T)fmin(fmax(st.rho, kRhoMin), kRhoMax) : a.rhos[b];
+            rho[gi] = fresh ? (T)fmin(fmax(st.rho, kRhoMin), kRhoMax) : a.rhos[b];
         }
 #pragma unroll
         for (int s = 0; s < NS; s++) xs[gi][s] = (load_state && s < KN) ? a.xs[(size_t)b * ncs + 4 * s + g] : T(0);
@@ -626,9 +652,18 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             y[gi][s] = (load_state && s < KM) ? a.ys[(size_t)b * mcs + 4 * s + g] : T(0);
         }
         rinv[gi] = T(1) / rho[gi];
+        cst[gi] = it;
     }
+    };
+    {
+        bool all[G];
+#pragma unroll
+        for (int gi = 0; gi < G; gi++) all[gi] = true;
+        load_cols(all, true);
     }
     it = __builtin_amdgcn_readfirstlane(it);  // lane 0 is always a live column; a phase shares `it`
+#pragma unroll
+    for (int gi = 0; gi < G; gi++) cst[gi] = 0;  // (a resumed phase counts from its QPs' saved `it`)
     MPCQ_PRO_MARK(3);
     T dk[G][NS];
     auto set_dk = [&]() {
@@ -689,10 +724,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             if (g == 0) {
                 a.rhos[b] = rho[gi];
                 a.status[b] = sta;
-                a.iter[b] = it;
+                a.iter[b] = it - cst[gi];
                 a.rho_out[b] = (double)rho[gi];
                 if (a.it_acc) {
-                    a.it_acc[b] += it;
+                    a.it_acc[b] += it - cst[gi];
                     a.uns_acc[b] += sta != kSolved;
                 }
             }
@@ -703,6 +738,58 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
 #pragma unroll
         for (int gi = 0; gi < G; gi++) d = d && done[gi];
         return wave_all(d);
+    };
+    // stream (STREAM), at a check iteration after the finalize: a column whose control step just
+    // finished advances its plant, X <- Ad X + Bd U + w (mpcq_plant_sim.h; lane g: components g, g + 4),
+    // and, while steps remain, starts the next step's QP in place (front end from the new X and U,
+    // warm state from the finalize's stores: the per-step path's arithmetic, bit for bit).  A column
+    // never waits for the others of its wave: each runs its own plant's steps.
+    int kst[G];    // the column's control steps finished
+    bool over[G];  // the column's plant has run all its steps (or the column is idle)
+#pragma unroll
+    for (int gi = 0; gi < G; gi++) {
+        kst[gi] = 0;
+        over[gi] = !valid[gi];
+    }
+    auto stream_next = [&]() {
+        if constexpr (refill) {
+            const int nx = a.nx;
+            for (;;) {
+                const bool fin = done[0] && !over[0];
+                if (!wave_any(fin)) return;
+                __threadfence_block();  // the finalize's U (lane g = 0) and state before they are read
+                const int b = b_[0];
+                double xv[8];
+#pragma unroll
+                for (int t = 0; t < 8; t++) xv[t] = (fin && t < nx) ? a.X[(size_t)b * nx + t] : 0.0;
+                const double uv = fin ? a.U[b] : 0.0;
+                const double *Ad = a.sim.Ad + (a.sim.shared ? 0 : (size_t)b * nx * nx);
+                const double *Bd = a.sim.Bd + (a.sim.shared ? 0 : (size_t)b * nx);
+                const unsigned long long key = sim_key(a.sim.seed), idx = (unsigned long long)(a.sim.first_qp + b);
+                const long long step = a.sim.first_step + kst[0];
+                double x0 = 0.0, x1 = 0.0;
+                if (fin && g < nx) x0 = sim_row(g, nx, Ad, Bd, xv, uv, key, idx, step, a.sim.noise_std);
+                if (fin && g + 4 < nx) x1 = sim_row(g + 4, nx, Ad, Bd, xv, uv, key, idx, step, a.sim.noise_std);
+                double *Xw = const_cast<double *>(a.X);
+                if (fin && g < nx) Xw[(size_t)b * nx + g] = x0;
+                if (fin && g + 4 < nx) Xw[(size_t)b * nx + g + 4] = x1;
+                __threadfence_block();  // the next step's front end reads X
+                bool fill[G];
+                fill[0] = fin && kst[0] + 1 < a.sim.steps;
+                if (fin) {
+                    kst[0] += 1;
+                    if (!fill[0]) over[0] = true;
+                }
+                if (!wave_any(fill[0])) return;
+                load_cols(fill, false);
+                set_dk();
+                bool bad[G];
+                bad[0] = fill[0] && status[0] != kUnsolved;
+                if (wave_any(bad[0])) finalize(bad, nullptr);
+                done[0] = fill[0] ? bad[0] : done[0];
+                if (!wave_any(bad[0])) return;  // (a step whose bounds were invalid: its plant advances again)
+            }
+        }
     };
 
     {
@@ -725,7 +812,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     const int ai = (st.adaptive_rho && a.adaptive_interval) ? a.adaptive_interval : 0;
     const int stop = a.stop_iter;
     int next_check = ct ? (it / ct + 1) * ct : -1;  // uniform; no integer division in the loop
-    int next_adapt = ai ? (it / ai + 1) * ai : -1;
+    // refill schedule: adapt_rho and max_iter fall on check iterations (host: multiples of ct) and are
+    // decided per column (its own iteration count); the wave schedules only the checks
+    const int ai_w = refill ? 0 : ai;
+    int next_adapt = ai_w ? (it / ai_w + 1) * ai_w : -1;
     T dx[G][NS], dy[G][MS];
     // paired loop: operators S, B~', B~ from the LDS images into VGPRs (A-fragment per tile, k-step)
     auto load_regs = [&](T (&rS)[NTR][KNR], T (&rBt)[NTR][KNR], T (&rB)[NTR][KNR]) {
@@ -962,9 +1052,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
         if constexpr (PAIRED) {
             // plain iterations up to the next info iteration, with the operators held in VGPRs
             // (loaded here, dead across the check code below)
-            int nxt = st.max_iter < stop ? st.max_iter : stop;
+            int nxt = refill ? next_check : (st.max_iter < stop ? st.max_iter : stop);
             if (ct && next_check < nxt) nxt = next_check;
-            if (ai && next_adapt < nxt) nxt = next_adapt;
+            if (ai_w && next_adapt < nxt) nxt = next_adapt;
             if (it + 1 < nxt) {
                 T rS[NTR][KNR], rBt[NTR][KNR], rB[NTR][KNR];
                 load_regs(rS, rBt, rB);
@@ -1008,11 +1098,29 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
 #define MPCQ_INFO_MARK(k) do { } while (0)
 #endif
         const bool at_check = it == next_check;
-        const bool at_adapt = it == next_adapt;
+        const bool at_adapt_w = it == next_adapt;
         if (at_check) next_check += ct;
-        if (at_adapt) next_adapt += ai;
-        const bool last = it == st.max_iter;
-        const bool info = at_check || at_adapt || last || it == stop;
+        if (at_adapt_w) next_adapt += ai_w;
+        const bool last_w = !refill && it == st.max_iter;
+        const bool info = at_check || at_adapt_w || last_w || it == stop;
+        // per column: adapt_rho and the end of the ADMM loop at the column's own iteration count
+        bool adapt_c[G], last_c[G];
+#pragma unroll
+        for (int gi = 0; gi < G; gi++) {
+            adapt_c[gi] = refill ? (at_check && ai && (it - cst[gi]) % ai == 0) : at_adapt_w;
+            last_c[gi] = refill ? (at_check && it - cst[gi] == st.max_iter) : last_w;
+        }
+        bool at_adapt = at_adapt_w, last = last_w;  // any column
+        if (refill && at_check) {
+            bool aa = false, ll = false;
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                aa = aa || (adapt_c[gi] && !done[gi]);
+                ll = ll || (last_c[gi] && !done[gi]);
+            }
+            at_adapt = wave_any(aa);
+            last = wave_any(ll);
+        }
 
         // ---- one ADMM iteration; the check iterations also keep delta_x', delta_y (OSQP's
         // delta_x / delta_y, for the infeasibility certificates)
@@ -1346,7 +1454,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
         if (at_adapt) {  // adapt_rho / compute_rho_estimate (scaled-space norms)
 #pragma unroll
             for (int gi = 0; gi < G; gi++) {
-                if (term[gi]) continue;
+                if (term[gi] || !adapt_c[gi]) continue;
                 const T pr = ax_z[gi] / (tt_max(zn_r[gi], axn_r[gi]) + T(kDivisionTol));
                 const T dn = tt_max(tt_max(qn_r[gi], atyn_r[gi]), pxn_r[gi]);
                 const T du = dr_r[gi] / (dn + T(kDivisionTol));
@@ -1363,19 +1471,19 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             int s1[G], s2[G];
 #pragma unroll
             for (int gi = 0; gi < G; gi++) {
-                need[gi] = !term[gi];
+                need[gi] = !term[gi] && last_c[gi];
                 s1[gi] = kUnsolved;
             }
             if (!at_check) check_termination(false, need, s1);
 #pragma unroll
             for (int gi = 0; gi < G; gi++) {
                 if (!term[gi] && s1[gi] != kUnsolved) { status[gi] = s1[gi]; term[gi] = true; }
-                need[gi] = !term[gi];
+                need[gi] = !term[gi] && last_c[gi];
             }
             check_termination(true, need, s2);
 #pragma unroll
             for (int gi = 0; gi < G; gi++)
-                if (!term[gi]) { status[gi] = s2[gi] != kUnsolved ? s2[gi] : kMaxIterReached; term[gi] = true; }
+                if (!term[gi] && last_c[gi]) { status[gi] = s2[gi] != kUnsolved ? s2[gi] : kMaxIterReached; term[gi] = true; }
         }
         MPCQ_INFO_MARK(4);
         {
@@ -1389,6 +1497,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
 #pragma unroll
             for (int gi = 0; gi < G; gi++) done[gi] = term[gi];
         }
+        if (refill && at_check) stream_next();
+        MPCQ_INFO_MARK(6);
         MPCQ_INFO_MARK(5);
 #if defined(MPCQ_INFO_STAMPS) && !defined(MPCQ_INFO_PART)
         if (a.stamps) info_cycles += (long long)__builtin_amdgcn_s_memtime() - t_info;
@@ -1444,15 +1554,17 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
 #endif
     };  // run_group
 
-    // this wave's 16 G QPs: slots wave_slot.. of the launch's list (or of the batch in phase 0)
-    const int wave_slot = (blk * WPB + (threadIdx.x >> 6)) * 16 * G;
+    // this wave's 16 G QPs: slots wave_slot.. of the launch's list (or of the batch in phase 0); a
+    // stream wave holds a.sim.cpw plants in its first columns
+    const int cpw = refill ? a.sim.cpw : 16 * G;
+    const int wave_slot = (blk * WPB + (threadIdx.x >> 6)) * cpw;
     if (wave_slot < count) {
         bool valid[G];
         int b_[G];
 #pragma unroll
         for (int gi = 0; gi < G; gi++) {
             const int slot = wave_slot + 16 * gi + c;
-            valid[gi] = slot < count;
+            valid[gi] = slot < count && (!refill || c < cpw);
             const int i = slot + (seglist ? seg * a.list_seg : 0);  // list entry
             b_[gi] = valid[gi] ? (seglist ? a.list_in[i] : a.qp0 + i) : 0;
         }
@@ -1470,6 +1582,23 @@ int tile_launch_variant(const AdmmArgs<T> &a, hipStream_t s)
     const int blocks = (a.batch + QPW - 1) / QPW;
     hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, AI, LF, G, OCC, PAIRED, WPB>), dim3(blocks), dim3(64 * WPB), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// The receding-horizon stream in one launch (AdmmArgs::sim): the paired condensed-MPC shape only
+// (-1 otherwise: the caller replays per-step launches).
+template <typename T, int KN, int KM>
+int tile_stream_launch(const AdmmArgs<T> &a, hipStream_t s)
+{
+    if constexpr (KM == 2 * KN) {
+        if (a.paired && a.all_ineq && a.lower_free) {
+            constexpr int OCC = 2, WPB = 4;  // (a stream is latency-bound: few waves, no spills)
+            const int waves = (a.batch + a.sim.cpw - 1) / a.sim.cpw;
+            hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 1, OCC, true, WPB, true>),
+                               dim3((waves + WPB - 1) / WPB), dim3(64 * WPB), 0, s, a);
+            return hipGetLastError() == hipSuccess ? 0 : -2;
+        }
+    }
+    return -1;
 }
 
 // One variant per shape and type (measured A/B): f32 runs one 16-QP group per
@@ -1494,6 +1623,15 @@ template <typename T>
 int tile_launch_any(const AdmmArgs<T> &a, int KN, int KM, hipStream_t s)
 {
 #define MPCQ_TRY(KN_, KM_) if (KN == KN_ && KM == KM_) return tile_launch<T, KN_, KM_>(a, s);
+    MPCQ_TILE_SHAPES(MPCQ_TRY)
+#undef MPCQ_TRY
+    return -1;
+}
+
+template <typename T>
+int tile_stream_launch_any(const AdmmArgs<T> &a, int KN, int KM, hipStream_t s)
+{
+#define MPCQ_TRY(KN_, KM_) if (KN == KN_ && KM == KM_) return tile_stream_launch<T, KN_, KM_>(a, s);
     MPCQ_TILE_SHAPES(MPCQ_TRY)
 #undef MPCQ_TRY
     return -1;

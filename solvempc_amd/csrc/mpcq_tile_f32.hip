@@ -5,3 +5,8 @@ extern "C" int mpcq_internal_tile_launch_f32(const mpcq::AdmmArgs<float> *a, int
 {
     return mpcq::tile_launch_any<float>(*a, KN, KM, s);
 }
+
+extern "C" int mpcq_internal_tile_stream_launch_f32(const mpcq::AdmmArgs<float> *a, int KN, int KM, hipStream_t s)
+{
+    return mpcq::tile_stream_launch_any<float>(*a, KN, KM, s);
+}

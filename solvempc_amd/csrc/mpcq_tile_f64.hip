@@ -5,3 +5,8 @@ extern "C" int mpcq_internal_tile_launch_f64(const mpcq::AdmmArgs<double> *a, in
 {
     return mpcq::tile_launch_any<double>(*a, KN, KM, s);
 }
+
+extern "C" int mpcq_internal_tile_stream_launch_f64(const mpcq::AdmmArgs<double> *a, int KN, int KM, hipStream_t s)
+{
+    return mpcq::tile_stream_launch_any<double>(*a, KN, KM, s);
+}

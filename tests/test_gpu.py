@@ -484,13 +484,17 @@ def test_receding_horizon_stream_f32(plant, kernel):
     assert len(tied) <= 2, tied
 
 
+@pytest.mark.parametrize("family", ["tile", "wave"])
 @pytest.mark.parametrize("dtype", ["f32", "f64"])
-def test_stream_one_launch_matches_graph(plant, dtype, monkeypatch):
-    """mpcq_mpc_run_device's one-launch stream (stream_wave_kernel: each wave runs its QP through all the
-    control steps) against the per-step hipGraph path (MPCQ_STREAM=graph) from the same cold state:
-    bit-identical X, U, statuses, iterations, rho and stream counters after 30 steps in one call,
-    then 7 more steps in a second call (warm state carried across calls), on a ragged batch."""
+def test_stream_one_launch_matches_graph(plant, dtype, family, monkeypatch):
+    """mpcq_mpc_run_device's one-launch stream against the per-step hipGraph path (MPCQ_STREAM=graph) of
+    the same kernel family, from the same cold state: the tile kernel's stream mode (every MFMA column
+    one plant running its own control steps, a few plants per wave) against per-step tile solves, and
+    stream_wave_kernel (one QP per wave) against per-step wave solves.  Bit-identical X, U, statuses,
+    iterations, rho and stream counters after 30 steps in one call, then 7 more steps in a second call
+    (warm state carried across calls), on a ragged batch."""
     import torch
+    monkeypatch.setenv("MPCQ_KERNEL", family)
     N, B = 20, 333
     ops = oracle.condense(plant, N)
     l = np.full(2 * N, LMIN)
@@ -515,6 +519,7 @@ def test_stream_one_launch_matches_graph(plant, dtype, monkeypatch):
             st.synchronize()
             it_acc, uns = s.stream_counters()
             out.append((Xd.cpu().numpy().copy(), Ud.cpu().numpy().copy(), *s.info(), it_acc, uns))
+            assert s.stream_path() == (mode or family)
         return out
 
     graph, one = run("graph"), run(None)
