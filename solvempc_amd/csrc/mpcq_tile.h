@@ -637,6 +637,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
 #pragma unroll
     for (int gi = 0; gi < G; gi++) {
         if (!fill[gi]) continue;
+        if (refill && !entry) {  // a stream column's next step: x', z, y, rho are in its registers
+            cst[gi] = it;
+            continue;
+        }
         const int b = b_[gi];
         if (resume) {
             rho[gi] = a.rhos[b];
@@ -685,6 +689,14 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     // ---- write the results of the `mine` QPs (OSQP store_solution / update_info; warm-start state)
     // Uold: U of each column read ahead of time (the info iteration prefetches it, so that U += x(0)
     // does not wait on a global load after the termination test), or null: read it here.
+    // stream (STREAM): per column, the control steps finished and whether its plant has run them all
+    int kst[G];    // the column's control steps finished
+    bool over[G];  // the column's plant has run all its steps (or the column is idle)
+#pragma unroll
+    for (int gi = 0; gi < G; gi++) {
+        kst[gi] = 0;
+        over[gi] = !valid[gi];
+    }
     auto finalize = [&](const bool (&mine)[G], const double *Uold) {
         // x = D W x'  (all lanes run the MFMA; `mine` lanes store)
         T xh[G][NS];
@@ -696,14 +708,31 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             const int b = opaque(b_[gi]);
             const int sta = status[gi];
             const bool has_sol = sta == kSolved || sta == kSolvedInaccurate || sta == kMaxIterReached;
+            // a stream column between two of its control steps keeps the solver state in registers
+            // (exactly what the next step would reload) and publishes only U; its last step writes all
+            const bool full = !refill || kst[gi] + 1 >= a.sim.steps;
 #pragma unroll
             for (int s = 0; s < NS; s++) {
                 const int v = 4 * s + g;
                 if (s < KN && v < n) {
                     const double xv = has_sol ? (double)xh[gi][s] * (double)s_D[v] : __builtin_nan("");
-                    if (a.x) a.x[(size_t)b * n + v] = xv;
+                    if (a.x && full) a.x[(size_t)b * n + v] = xv;
                     if (v == 0 && a.mpc_u && sta == kSolved) a.U[b] = (Uold ? Uold[gi] : a.U[b]) + xv;  // U += x(0)  (:105)
                 }
+            }
+            const bool keep = has_sol || sta == kInvalidBounds || sta == kTypeChanged;
+            if (!full) {
+                if (!keep) {
+#pragma unroll
+                    for (int s = 0; s < NS; s++) xs[gi][s] = T(0);
+#pragma unroll
+                    for (int s = 0; s < MS; s++) z[gi][s] = y[gi][s] = T(0);
+                }
+                if (g == 0 && a.it_acc) {
+                    a.it_acc[b] += it - cst[gi];
+                    a.uns_acc[b] += sta != kSolved;
+                }
+                continue;
             }
 #pragma unroll
             for (int s = 0; s < MS; s++) {
@@ -711,7 +740,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 if (s < KM && v < m && a.y)
                     a.y[(size_t)b * m + v] = has_sol ? ((double)y[gi][s] * (double)s_E[v]) * cinv64 : __builtin_nan("");
             }
-            const bool keep = has_sol || sta == kInvalidBounds || sta == kTypeChanged;
 #pragma unroll
             for (int s = 0; s < NS; s++)
                 if (s < KN) a.xs[(size_t)b * ncs + 4 * s + g] = keep ? xs[gi][s] : T(0);
@@ -744,13 +772,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     // and, while steps remain, starts the next step's QP in place (front end from the new X and U,
     // warm state from the finalize's stores: the per-step path's arithmetic, bit for bit).  A column
     // never waits for the others of its wave: each runs its own plant's steps.
-    int kst[G];    // the column's control steps finished
-    bool over[G];  // the column's plant has run all its steps (or the column is idle)
-#pragma unroll
-    for (int gi = 0; gi < G; gi++) {
-        kst[gi] = 0;
-        over[gi] = !valid[gi];
-    }
     auto stream_next = [&]() {
         if constexpr (refill) {
             const int nx = a.nx;
