@@ -126,6 +126,33 @@ template <typename T> __device__ __forceinline__ T col_sum(T v)
 {
     return col_reduce(v, [](T a, T b) { return a + b; });
 }
+// The values of the other lanes of this lane's column: v of lane group g ^ 1 (v_permlane16_swap pairs
+// rows 0-1 and 2-3) and g ^ 2 (v_permlane32_swap pairs rows 0-2 and 1-3); a swap of v with itself
+// leaves {own, partner} in even rows / halves and {partner, own} in odd ones.
+__device__ __forceinline__ double col_x16(double v, int g)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+    auto r = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    const int k = (g & 1) ? 0 : 1;
+    return __longlong_as_double((long long)(((unsigned long long)h[k] << 32) | r[k]));
+}
+__device__ __forceinline__ double col_x32(double v, int g)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+    auto r = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    const int k = (g & 2) ? 0 : 1;
+    return __longlong_as_double((long long)(((unsigned long long)h[k] << 32) | r[k]));
+}
+// v of lane group `src` of this column, on every lane of the column (moves only: bit-exact)
+__device__ __forceinline__ double col_from(double v, int src, int g)
+{
+    const double v1 = col_x16(v, g), v2 = col_x32(v, g), v3 = col_x32(v1, g);
+    return src == g ? v : (src == (g ^ 1) ? v1 : (src == (g ^ 2) ? v2 : v3));
+}
 __device__ __forceinline__ int col_or(int v)
 {
     return (int)swap_combine((unsigned)v, [](unsigned a, unsigned b) { return a | b; });
@@ -509,6 +536,17 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     T rho[G], rinv[G];
     int it = 0;
     int cst[G];  // the wave iteration the column's QP started at (its own iteration: it - cst)
+    // stream (STREAM): per column, the control steps finished and whether its plant has run them all
+    int kst[G];    // the column's control steps finished
+    bool over[G];  // the column's plant has run all its steps (or the column is idle)
+#pragma unroll
+    for (int gi = 0; gi < G; gi++) {
+        kst[gi] = 0;
+        over[gi] = !valid[gi];
+    }
+    double sX[8], sU = 0.0;  // stream: the column's plant state X, U (every lane of the column holds it)
+#pragma unroll
+    for (int t = 0; t < 8; t++) sX[t] = 0.0;
     // ---- per-QP data of the columns in `fill` (element v = 4 s + g of this lane's QP column), per
     // group: every column at entry, the refilled ones at a check (the others keep their registers and
     // reproduce their W' q^ bit for bit).  Every global load of a group is issued (index clamped into
@@ -518,18 +556,31 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
 #pragma unroll
     for (int gi = 0; gi < G; gi++) {
         const int b = b_[gi];
-        const bool pub = valid[gi] && fill[gi];  // this column's QP is (re)loaded: publish its outputs
+        // this column's QP is (re)loaded: publish its outputs (a stream column: at its last step)
+        const bool pub = valid[gi] && fill[gi] && (!refill || kst[gi] + 1 >= a.sim.steps);
         double qk[KN], up[KM], lo[LFREE ? 1 : KM];
         if (fe_on) {  // setF (:372-375) q = Fx X + Fu U + Fr ref;  (:93-99) u = W0 + Sbar X + Ku U
             // (a resumed phase recomputes them: X is read-only and U changes only at a QP's finalize)
             double Xv[8];
             const int nx = a.nx;
+            double Uv;
+            if (refill && !entry) {  // a stream column's later step: its plant state is in registers
 #pragma unroll
-            for (int t = 0; t < 8; t++) Xv[t] = a.X[(size_t)b * nx + (t < nx ? t : 0)];
-            const double Uv = a.U[b];
+                for (int t = 0; t < 8; t++) Xv[t] = sX[t];
+                Uv = sU;
+            } else {
 #pragma unroll
-            for (int t = 0; t < 8; t++)
-                if (t >= nx) Xv[t] = 0.0;
+                for (int t = 0; t < 8; t++) Xv[t] = a.X[(size_t)b * nx + (t < nx ? t : 0)];
+                Uv = a.U[b];
+#pragma unroll
+                for (int t = 0; t < 8; t++)
+                    if (t >= nx) Xv[t] = 0.0;
+                if (refill) {
+#pragma unroll
+                    for (int t = 0; t < 8; t++) sX[t] = Xv[t];
+                    sU = Uv;
+                }
+            }
 #pragma unroll
             for (int s = 0; s < KN; s++) {
                 const int v = 4 * s + g;  // < NCP: padded rows of fe are zero
@@ -542,8 +593,19 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 if (mpc_fe && a.q_out && pub && v < n) a.q_out[(size_t)b * n + v] = qk[s];
             }
             if (mpc_fe && a.X_save && pub) {  // the step's X, U: q, u on demand (materialize_qu)
-                if (g < nx) a.X_save[(size_t)b * nx + g] = a.X[(size_t)b * nx + g];  // (cache-hot reloads:
-                if (g + 4 < nx) a.X_save[(size_t)b * nx + g + 4] = a.X[(size_t)b * nx + g + 4];  // no register index by lane)
+                if (refill) {  // (selects: no register index by lane)
+                    double x0 = 0.0, x1 = 0.0;
+#pragma unroll
+                    for (int t = 0; t < 4; t++) {
+                        x0 = t == g ? Xv[t] : x0;
+                        x1 = t == g ? Xv[t + 4] : x1;
+                    }
+                    if (g < nx) a.X_save[(size_t)b * nx + g] = x0;
+                    if (g + 4 < nx) a.X_save[(size_t)b * nx + g + 4] = x1;
+                } else {
+                    if (g < nx) a.X_save[(size_t)b * nx + g] = a.X[(size_t)b * nx + g];  // (cache-hot reloads:
+                    if (g + 4 < nx) a.X_save[(size_t)b * nx + g + 4] = a.X[(size_t)b * nx + g + 4];  // no register index by lane)
+                }
                 if (g == 0) a.U_save[b] = Uv;
             }
             MPCQ_PRO_MARK(11);
@@ -689,14 +751,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     // ---- write the results of the `mine` QPs (OSQP store_solution / update_info; warm-start state)
     // Uold: U of each column read ahead of time (the info iteration prefetches it, so that U += x(0)
     // does not wait on a global load after the termination test), or null: read it here.
-    // stream (STREAM): per column, the control steps finished and whether its plant has run them all
-    int kst[G];    // the column's control steps finished
-    bool over[G];  // the column's plant has run all its steps (or the column is idle)
-#pragma unroll
-    for (int gi = 0; gi < G; gi++) {
-        kst[gi] = 0;
-        over[gi] = !valid[gi];
-    }
     auto finalize = [&](const bool (&mine)[G], const double *Uold) {
         // x = D W x'  (all lanes run the MFMA; `mine` lanes store)
         T xh[G][NS];
@@ -717,8 +771,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 if (s < KN && v < n) {
                     const double xv = has_sol ? (double)xh[gi][s] * (double)s_D[v] : __builtin_nan("");
                     if (a.x && full) a.x[(size_t)b * n + v] = xv;
-                    if (v == 0 && a.mpc_u && sta == kSolved) a.U[b] = (Uold ? Uold[gi] : a.U[b]) + xv;  // U += x(0)  (:105)
+                    if (!refill && v == 0 && a.mpc_u && sta == kSolved) a.U[b] = (Uold ? Uold[gi] : a.U[b]) + xv;  // U += x(0)  (:105)
                 }
+            }
+            if (refill) {  // stream: U += x(0) on every lane of the column (x(0): lane group 0, register 0)
+                const double x0 = col_from(has_sol ? (double)xh[gi][0] * (double)s_D[0] : 0.0, 0, g);
+                if (a.mpc_u && sta == kSolved) sU = sU + x0;
+                if (full && g == 0) a.U[b] = sU;
             }
             const bool keep = has_sol || sta == kInvalidBounds || sta == kTypeChanged;
             if (!full) {
@@ -778,28 +837,30 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             for (;;) {
                 const bool fin = done[0] && !over[0];
                 if (!wave_any(fin)) return;
-                __threadfence_block();  // the finalize's U (lane g = 0) and state before they are read
                 const int b = b_[0];
-                double xv[8];
-#pragma unroll
-                for (int t = 0; t < 8; t++) xv[t] = (fin && t < nx) ? a.X[(size_t)b * nx + t] : 0.0;
-                const double uv = fin ? a.U[b] : 0.0;
                 const double *Ad = a.sim.Ad + (a.sim.shared ? 0 : (size_t)b * nx * nx);
                 const double *Bd = a.sim.Bd + (a.sim.shared ? 0 : (size_t)b * nx);
                 const unsigned long long key = sim_key(a.sim.seed), idx = (unsigned long long)(a.sim.first_qp + b);
                 const long long step = a.sim.first_step + kst[0];
                 double x0 = 0.0, x1 = 0.0;
-                if (fin && g < nx) x0 = sim_row(g, nx, Ad, Bd, xv, uv, key, idx, step, a.sim.noise_std);
-                if (fin && g + 4 < nx) x1 = sim_row(g + 4, nx, Ad, Bd, xv, uv, key, idx, step, a.sim.noise_std);
-                double *Xw = const_cast<double *>(a.X);
-                if (fin && g < nx) Xw[(size_t)b * nx + g] = x0;
-                if (fin && g + 4 < nx) Xw[(size_t)b * nx + g + 4] = x1;
-                __threadfence_block();  // the next step's front end reads X
+                if (fin && g < nx) x0 = sim_row(g, nx, Ad, Bd, sX, sU, key, idx, step, a.sim.noise_std);
+                if (fin && g + 4 < nx) x1 = sim_row(g + 4, nx, Ad, Bd, sX, sU, key, idx, step, a.sim.noise_std);
+                // the new X on every lane of the column (component t from lane group t & 3)
+#pragma unroll
+                for (int t = 0; t < 8; t++) {
+                    const double v = col_from(t < 4 ? x0 : x1, t & 3, g);
+                    if (fin) sX[t] = t < nx ? v : 0.0;
+                }
                 bool fill[G];
                 fill[0] = fin && kst[0] + 1 < a.sim.steps;
                 if (fin) {
                     kst[0] += 1;
                     if (!fill[0]) over[0] = true;
+                }
+                if (fin && !fill[0]) {  // the plant's last step: its final X (U: the finalize)
+                    double *Xw = const_cast<double *>(a.X);
+                    if (g < nx) Xw[(size_t)b * nx + g] = x0;
+                    if (g + 4 < nx) Xw[(size_t)b * nx + g + 4] = x1;
                 }
                 if (!wave_any(fill[0])) return;
                 load_cols(fill, false);
@@ -1203,7 +1264,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
         iterate(std::true_type{});
         double Uold[G];  // U of the running columns, ahead of a finalize (latency hidden by the checks)
 #pragma unroll
-        for (int gi = 0; gi < G; gi++) Uold[gi] = (a.mpc_u && g == 0 && !done[gi]) ? a.U[opaque(b_[gi])] : 0.0;
+        for (int gi = 0; gi < G; gi++) Uold[gi] = (!refill && a.mpc_u && g == 0 && !done[gi]) ? a.U[opaque(b_[gi])] : 0.0;
         MPCQ_INFO_MARK(1);
 #pragma unroll
         for (int gi = 0; gi < G; gi++)
