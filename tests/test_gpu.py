@@ -529,6 +529,44 @@ def test_stream_one_launch_matches_graph(plant, dtype, family, monkeypatch):
     assert np.all(one[-1][2] == sm.SOLVED) and one[-1][6].sum() == 0  # (X, U, status, iter, rho, it_acc, uns)
 
 
+@pytest.mark.parametrize("over", [dict(max_iter=50), dict(check_termination=10), dict(adaptive_rho=0),
+                                  dict(max_iter=30, check_termination=7)],
+                         ids=["max_iter50", "check10", "no_adapt", "max_iter30_check7"])
+def test_stream_tile_settings_variants(plant, over, monkeypatch):
+    """The tile stream mode under OSQP settings the reference could set (:51-52): per-column max_iter
+    (MAX_ITER_REACHED / SOLVED_INACCURATE steps), another check interval, no adaptive rho, bit-identical
+    to per-step tile solves; settings whose max_iter or adapt interval is off the check grid
+    (max_iter 30, check 7) run the per-step launches instead, with the same results."""
+    import torch
+    monkeypatch.setenv("MPCQ_KERNEL", "tile")
+    N, B, steps = 20, 200, 20
+    ops = oracle.condense(plant, N)
+    l = np.full(2 * N, LMIN)
+    X, U = workload.stream_states(4, 0, B)
+    settings = sm.default_settings(**over)
+
+    def run(mode):
+        if mode:
+            monkeypatch.setenv("MPCQ_STREAM", mode)
+        else:
+            monkeypatch.delenv("MPCQ_STREAM", raising=False)
+        s = sm.BatchSolver(N, 2 * N, B, dtype="f32", settings=settings)
+        s.setup(ops["P"], np.zeros(N), ops["A"], l, oracle.upper_bound(ops, np.zeros(4), 0.0))
+        s.mpc_set_operators(ops["Fx"], ops["Fu"], ops["Fr"], ops["Sbar"], ops["Ku"], ops["W0"])
+        s.mpc_set_plant(plant["Ad"], plant["Bd"])
+        Xd, Ud = torch.from_numpy(X.copy()).cuda(), torch.from_numpy(U.copy()).cuda()
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            s.mpc_run_device(Xd.data_ptr(), Ud.data_ptr(), 0.0, steps, 4, 0, 0, 1e-2, st.cuda_stream)
+        st.synchronize()
+        return s.stream_path(), (Xd.cpu().numpy(), Ud.cpu().numpy(), *s.info(), *s.stream_counters())
+
+    (pg, g), (po, o) = run("graph"), run(None)
+    assert pg == "graph" and po == ("graph" if over.get("check_termination") == 7 else "tile")
+    for a_, b_ in zip(g, o):
+        assert np.array_equal(a_, b_)
+
+
 def test_stream_workload_stays_solved_and_bounded(plant):
     """The config-5 workload (workload.stream_states, noise std 1e-2) over 400 fp32 control steps: every
     plant SOLVED at every step and the closed loop bounded (the reference controller on its plant)."""
