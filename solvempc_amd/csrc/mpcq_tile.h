@@ -885,6 +885,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             finalize(mine, nullptr);
 #pragma unroll
             for (int gi = 0; gi < G; gi++) done[gi] = done[gi] || mine[gi];
+            // a stream column whose first step failed at once advances now (a wave whose columns all
+            // failed would otherwise never reach a check)
+            if constexpr (refill) stream_next();
         }
     }
 

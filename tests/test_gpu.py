@@ -567,6 +567,45 @@ def test_stream_tile_settings_variants(plant, over, monkeypatch):
         assert np.array_equal(a_, b_)
 
 
+def test_stream_failed_steps_advance(plant, monkeypatch):
+    """Stream plants whose every step fails OSQP's bound update (a state so large that u^ passes
+    OSQP_INFTY * MIN_SCALING: TYPE_CHANGED, U unchanged) still advance their plant each step, also when
+    every plant of a wave fails from the start (4 plants per wave, the first wave all failing): the tile
+    stream mode against per-step tile solves, bit for bit."""
+    import torch
+    monkeypatch.setenv("MPCQ_KERNEL", "tile")
+    monkeypatch.setenv("MPCQ_STREAM_CPW", "4")
+    N, B, steps = 20, 8, 5
+    ops = oracle.condense(plant, N)
+    l = np.full(2 * N, LMIN)
+    X, U = workload.stream_states(4, 0, B)
+    X[:4] *= 1e29
+
+    def run(mode):
+        if mode:
+            monkeypatch.setenv("MPCQ_STREAM", mode)
+        else:
+            monkeypatch.delenv("MPCQ_STREAM", raising=False)
+        s = sm.BatchSolver(N, 2 * N, B, dtype="f32")
+        s.setup(ops["P"], np.zeros(N), ops["A"], l, oracle.upper_bound(ops, np.zeros(4), 0.0))
+        s.mpc_set_operators(ops["Fx"], ops["Fu"], ops["Fr"], ops["Sbar"], ops["Ku"], ops["W0"])
+        s.mpc_set_plant(plant["Ad"], plant["Bd"])
+        Xd, Ud = torch.from_numpy(X.copy()).cuda(), torch.from_numpy(U.copy()).cuda()
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            s.mpc_run_device(Xd.data_ptr(), Ud.data_ptr(), 0.0, steps, 4, 0, 0, 1e-2, st.cuda_stream)
+        st.synchronize()
+        return s.stream_path(), (Xd.cpu().numpy(), Ud.cpu().numpy(), *s.info(), *s.stream_counters())
+
+    (pg, g), (po, o) = run("graph"), run(None)
+    assert pg == "graph" and po == "tile"
+    for a_, b_ in zip(g, o):
+        assert np.array_equal(a_, b_)
+    assert np.all(o[2][:4] == sm.TYPE_CHANGED) and np.all(o[2][4:] == sm.SOLVED)
+    assert np.all(o[6][:4] == steps) and np.all(o[6][4:] == 0)  # unsolved steps per plant
+    assert not np.array_equal(o[0][:4], X[:4])  # the failing plants still moved
+
+
 def test_stream_workload_stays_solved_and_bounded(plant):
     """The config-5 workload (workload.stream_states, noise std 1e-2) over 400 fp32 control steps: every
     plant SOLVED at every step and the closed loop bounded (the reference controller on its plant)."""
