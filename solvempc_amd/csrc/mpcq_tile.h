@@ -1383,6 +1383,15 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
 
         // OSQP is_primal_infeasible on delta_y = dy (this iteration's dual step), per group.
         auto primal_infeasible = [&](T eps, const bool (&need)[G], bool (&res)[G]) {
+            {  // no column of the wave asks (every live one primal-feasible): nothing to screen
+                bool anyn = false;
+#pragma unroll
+                for (int gi = 0; gi < G; gi++) {
+                    res[gi] = false;
+                    anyn = anyn || need[gi];
+                }
+                if (!wave_any(anyn)) return;
+            }
             T d[G][MS];
             T ndy[G], lhs[G];
             const T *E = fresh_ptr((const T *)s_E);
