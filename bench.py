@@ -249,7 +249,7 @@ def main_quadrotor(a, rank, world, local, dist, dev):
                   "solved_frac": float(np.mean(status == sm.SOLVED)), "rho_adapted_frac": float(np.mean(fact > 1))},
         "collective": _collective(dist, world, got),
     })
-    if a.cpu_seconds > 0:
+    if a.cpu_seconds > 0 and world == 1:  # (rank 0 at N = 1 only)
         import oracle
 
         run = lambda n, t: oracle.mimo_plants_step(sh, Ad[:n], Bd[:n], X[:n], U[:n], N, nthreads=t)  # noqa: E731
@@ -536,7 +536,7 @@ def main_lti(a, rank, world, local, dist, dev):
                            "dense_equivalent": {"flops_per_step": flops_dense + B * workload.flops_plant_setup(N, 2 * N),
                                                 "note": "SURVEY §8d: dense F_iter / F_check + F_condense + Ruiz + one LDL"}}
         rec["iters"]["rho_adapted_frac"] = float(refac.mean())
-    if a.cpu_seconds > 0 and not stream_mode:
+    if a.cpu_seconds > 0 and not stream_mode and world == 1:  # (rank 0 at N = 1 only)
         import oracle
 
         if perplant:
