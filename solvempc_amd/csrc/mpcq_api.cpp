@@ -43,6 +43,9 @@ constexpr int kMaxPhases = 16;
 //   MPCQ_SETUP=ref              per-plant setup on the workgroup kernel (mpcq_setup.hip)
 //   MPCQ_CONDENSE=ref           condensing on the workgroup kernel (mpcq_condense.hip)
 //   MPCQ_MIMO_GENERAL_K0=1      the MIMO solve's general-K0 exchange path on a diagonal K0
+//   MPCQ_STREAM=graph|wave      mpcq_mpc_run_device's per-step graph or one-QP-per-wave launch
+//                               (mpcq_get_stream_path reports the choice)
+//   MPCQ_STREAM_CPW=k           plants per wave of the tile stream mode
 // Debug builds (-DMPCQ_DEBUG_HOOKS) add the stamp / profiling dumps (MPCQ_TILE_STAMPS,
 // MPCQ_SETUP_PROF, MPCQ_MIMO_SETUP_STAMPS, MPCQ_MIMO_STAMPS) and MPCQ_DEBUG_SYNC.
 const char *test_hook(const char *name)
