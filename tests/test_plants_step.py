@@ -106,3 +106,29 @@ def test_one_shot_context_contract(plant):
     with pytest.raises(sm.MpcqError) as e:
         s.solve()
     assert e.value.code == _capi.MPCQ_ERR_ORDER
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_full_config3_batch_every_plant(plant, dtype):
+    """The bench's config-3 batch at its size (131,072 randomised plants, seed 2) against the oracle on
+    every plant (OpenMP over the host cores, ~2 s on the GPU box), under the module's bar."""
+    N, B = 20, 131072
+    Ad, Bd, X, U = _plants(plant, B, 2)
+    s, Ug = _fused(plant, Ad, Bd, X, U, N, dtype)
+    st, it, _ = s.info()
+    U_ref, st_ref, it_ref, x_ref, margin = oracle.plants_step(plant, Ad, Bd, X, U, N, full=True)
+    assert np.array_equal(st, st_ref) and np.all(st == sm.SOLVED)
+    x = s.solution()
+    if dtype == "f64":
+        assert np.array_equal(it, it_ref)
+        assert np.abs(Ug - U_ref).max() < 1e-9 and np.abs(x - x_ref).max() < 1e-9
+        return
+    off = it != it_ref
+    assert not np.any(off & (margin >= TIE_MARGIN)), (np.flatnonzero(off)[:8], margin[off][:8])
+    scale = np.maximum(1.0, np.abs(x_ref).max(axis=1))
+    assert (np.abs(x - x_ref).max(axis=1)[~off] / scale[~off]).max() < 1e-5
+    assert (np.abs(Ug - U_ref)[~off] / scale[~off]).max() < 1e-5
+    # a tie's other branch stops one check earlier or later: an OSQP answer at eps_abs = eps_rel = 1e-3
+    # of its own, within the eps-level gap of the oracle's (SURVEY App. B: up to ~2e-2)
+    assert (np.abs(x - x_ref).max(axis=1)[off] / scale[off]).max(initial=0.0) < 5e-2
+    print(f"fp32 config 3: {int(off.sum())} of {B} plants took a tie's other branch")
