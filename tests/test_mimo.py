@@ -173,3 +173,16 @@ def test_nonconvex_plant_fails_setup():
     X, U = workload.quadrotor_states(3, 0, B)
     with pytest.raises(sm.MpcqError, match="not positive definite"):
         _run_device(sh, Ad, Bd, X, U, N)
+
+
+def test_quadrotor_bench_sample_matches_oracle():
+    """4,096 plants of the config-4 bench batch (seed 3, its first plants; the oracle does ~500 of these
+    per second per host share, so the full 262,144 are out of reach here) under the module's bar."""
+    N, B = 30, 4096
+    Ad, Bd = workload.quadrotor_plants(3, 0, B)
+    sh = workload.quadrotor_shared()
+    X, U = workload.quadrotor_states(3, 0, B)
+    Us, x, st, it = _run_device(sh, Ad, Bd, X, U, N)
+    U_ref, x_ref, st_ref, it_ref, mg = oracle.mimo_plants_step(sh, Ad, Bd, X, U, N, margins=True)
+    assert np.all(st == sm.SOLVED)
+    _check(x, st, it, Us[0], x_ref, st_ref, it_ref, U_ref, mg)
