@@ -150,17 +150,20 @@ def _parity(du0_gpu, it_gpu, x_ref, it_ref, st_ref) -> dict:
             "max_abs_du0": float(d.max()), "max_rel_du0": float((d / scale).max())}
 
 
-def cpu_baseline(kind: str, run, n0: int, total: int, budget: float, threads: int, what: str):
+def cpu_baseline(kind: str, run, n0: int, total: int, budget: float, threads: int, what: str,
+                 per_unit: int = 1):
     """Time the oracle (`run(n, nthreads)`) single-threaded and on `threads` OpenMP threads over a
-    bounded prefix of the same batch; returns the record and the multi-threaded run's results."""
+    bounded prefix of the same batch (n units of `per_unit` QP solves each); returns the record and
+    the multi-threaded run's results."""
     info = cpu_info()
     thr = threads or info["threads"]
-    n1, dt1, _ = _timed(lambda n: run(n, 1), max(8, n0 // 16), total, budget / 2)
+    n1, dt1, _ = _timed(lambda n: run(n, 1), max(1 if per_unit > 1 else 8, n0 // 16), total, budget / 2)
     n, dt, res = _timed(lambda n: run(n, thr), n0, total, budget / 2)
-    rec = {"value": n / dt, "unit": "QP/s", "cores": thr, "kind": kind,
-           "single_thread": {"value": n1 / dt1, "sample": f"{n1} QPs, {dt1:.2f} s"},
+    unit = "QPs" if per_unit == 1 else f"plants x {per_unit} steps"
+    rec = {"value": n * per_unit / dt, "unit": "QP/s", "cores": thr, "kind": kind,
+           "single_thread": {"value": n1 * per_unit / dt1, "sample": f"{n1} {unit}, {dt1:.2f} s"},
            "cpu": info,
-           "sample": f"{n} of the batch's QPs (its first {n}): {what}, fp64, OpenMP {thr} threads, {dt:.2f} s"}
+           "sample": f"{n} {unit} of the batch (its first {n}): {what}, fp64, OpenMP {thr} threads, {dt:.2f} s"}
     return rec, n, res
 
 
@@ -536,6 +539,22 @@ def main_lti(a, rank, world, local, dist, dev):
                            "dense_equivalent": {"flops_per_step": flops_dense + B * workload.flops_plant_setup(N, 2 * N),
                                                 "note": "SURVEY §8d: dense F_iter / F_check + F_condense + Ruiz + one LDL"}}
         rec["iters"]["rho_adapted_frac"] = float(refac.mean())
+    if a.cpu_seconds > 0 and stream_mode and world == 1:  # (rank 0 at N = 1 only)
+        import oracle
+
+        run = lambda n, t: oracle.stream_run(plant, X[:n], U[:n], N, a.ctrl_steps, a.seed, start, 0, a.noise,  # noqa: E731
+                                             xref=plant["xref"], nthreads=t)
+        rec["cpu_baseline"], ns, (Xc, Uc, itc, unc) = cpu_baseline(
+            "port", run, 16, B, a.cpu_seconds, a.cpu_threads,
+            "oracle/mpc_batch.c ora_stream_run (one warm-started OSQP-0.6 restatement per plant, the device's "
+            "noise stream)", per_unit=a.ctrl_steps)
+        # the device's last bench step on the same plants (informational: fp32 and fp64 closed loops
+        # drift apart by rounding over the steps, each step's parity is tests/test_gpu.py's)
+        rec["parity"] = {"plants": int(ns), "steps": a.ctrl_steps,
+                         "it_total_match": float(np.mean(it_total[:ns] == itc)),
+                         "it_total_rel_diff": float(np.abs(it_total[:ns] - itc).sum() / max(1, itc.sum())),
+                         "max_abs_dU_final": float(np.abs(U_d[:ns].cpu().numpy() - Uc).max()),
+                         "unsolved_steps_cpu": int(unc.sum())}
     if a.cpu_seconds > 0 and not stream_mode and world == 1:  # (rank 0 at N = 1 only)
         import oracle
 

@@ -116,6 +116,10 @@ def lib() -> C.CDLL:
     L.ora_plants_step.restype = C.c_int
     L.ora_plants_step.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, dp, dp, dp, dp, C.c_double, C.c_double,
                                   C.c_double, dp, dp, C.c_double, C.POINTER(Settings), dp, ip, ip, C.c_int, dp, dp]
+    L.ora_stream_run.restype = C.c_int
+    L.ora_stream_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, dp, dp, dp, dp, C.c_double, C.c_double,
+                                 C.c_double, dp, dp, C.c_double, C.POINTER(Settings), C.c_int, C.c_ulonglong,
+                                 C.c_longlong, C.c_longlong, C.c_double, ip, ip, C.c_int]
     L.ora_condense_mimo.restype = C.c_int
     L.ora_condense_mimo.argtypes = [C.POINTER(_MimoPlant), C.POINTER(_MimoOps)]
     L.ora_mimo_plants_step.restype = C.c_int
@@ -380,3 +384,23 @@ def kkt_residuals(P, q, A, l, u, x, y) -> dict:
         "dual_sign": float(dual_sign.max(initial=0.0)),
         "complementarity": float(compl.max(initial=0.0)),
     }
+
+
+def stream_run(plant: dict, X, U, N: int, steps: int, seed: int, first_qp: int = 0, first_step: int = 0,
+               noise_std: float = 1e-2, s_rows: int = 10, xref: float = 0.0, settings: Settings | None = None,
+               nthreads: int = 0):
+    """Config 5 on the CPU (oracle/mpc_batch.c ora_stream_run): every plant a copy of `plant` with its own
+    warm-started solver, `steps` [controllerStep; plant update] rounds on the device's noise stream.
+    Returns (X, U after the steps, per-plant iterations summed over the steps, unsolved steps)."""
+    X, U = _c64(X).copy(), _c64(U).copy()
+    k, nx = X.shape
+    s = settings or default_settings()
+    it = np.zeros(k, dtype=np.int32)
+    un = np.zeros(k, dtype=np.int32)
+    Ad, Bd, Cd, K = (_c64(plant[key]) for key in ("Ad", "Bd", "Cd", "K"))
+    rc = lib().ora_stream_run(k, nx, N, s_rows, _dp(Ad), _dp(Bd), _dp(Cd), _dp(K), plant["Q"], plant["R"],
+                              plant["RD"], _dp(X), _dp(U), xref, C.byref(s), steps, seed, first_qp, first_step,
+                              noise_std, _ip(it), _ip(un), nthreads)
+    if rc < 0:
+        raise ValueError("ora_stream_run: setup rejected the plant")
+    return X, U, it, un

@@ -204,3 +204,27 @@ def test_stream_workload_closed_loop_is_bounded():
                     assert not bounded
             X = workload.simulate(plant["Ad"], plant["Bd"], X, U, workload.plant_noise(4, 0, B, k, 4, 1e-2))
         assert (np.abs(X).max() < 10) == bounded, (law, np.abs(X).max())
+
+
+def test_stream_run_matches_python_replay(plant):
+    """oracle.stream_run (the config-5 CPU baseline: one warm-started solver per plant, the device's
+    noise stream) against a step-by-step replay with oracle.Solver and workload.simulate."""
+    N, B, steps = 20, 5, 10
+    X, U = workload.stream_states(4, 0, B)
+    Xc, Uc, it, un = oracle.stream_run(plant, X, U, N, steps, 4, 0, 0, 1e-2)
+    ops = oracle.condense(plant, N)
+    l = np.full(2 * N, -np.finfo(np.float64).max)
+    refs = [oracle.Solver(ops["P"], np.zeros(N), ops["A"], l, oracle.upper_bound(ops, np.zeros(4), 0.0))
+            for _ in range(B)]
+    Xk, Uk, its = X.copy(), U.copy(), np.zeros(B, dtype=np.int64)
+    for k in range(steps):
+        for b, r in enumerate(refs):
+            assert r.update_gradient(oracle.gradient(ops, Xk[b], Uk[b]))
+            assert r.update_upper_bound(oracle.upper_bound(ops, Xk[b], Uk[b]))
+            if r.solve() == oracle.SOLVED:
+                Uk[b] += r.x()[0]
+            its[b] += r.info().iter
+        Xk = workload.simulate(plant["Ad"], plant["Bd"], Xk, Uk, workload.plant_noise(4, 0, B, k, 4, 1e-2))
+    assert np.array_equal(it, its) and np.all(un == 0)
+    np.testing.assert_allclose(Uc, Uk, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(Xc, Xk, rtol=0, atol=1e-12)
