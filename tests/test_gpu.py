@@ -993,3 +993,32 @@ def test_formulations_do_not_mix(plant):
     s.mpc_step_device(Xd.data_ptr(), Ud.data_ptr())  # the generic formulation runs
     torch.cuda.synchronize()
     assert np.all(s.info()[0] == sm.SOLVED)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_difficulty_order_is_bit_identical(plant, dtype, monkeypatch):
+    """With MPCQ_ORDER=1 the tile path's first phase takes the QPs in difficulty order (mpcq_order.hip):
+    only the wave a QP runs in changes, so the generic solve and the controllerStep path give
+    bit-identical solutions, duals, statuses and iteration counts in index and difficulty order, and
+    two ordered solves agree bit for bit although the order inside a bin is set by atomics.  (This is
+    also the check that a QP's arithmetic does not depend on the other columns of its wave.)"""
+    import torch
+    N, B = 20, 16384
+    ops, X, U, q, u = _problem(plant, N, B, seed=31)
+    l = np.full(2 * N, LMIN)
+    res = {}
+    for order in ("0", "1", "1b"):
+        monkeypatch.setenv("MPCQ_ORDER", order[0])
+        s = _gpu_solve(ops, q, u, N, dtype=dtype)
+        gen = (s.solution(), s.dual(), *s.info())
+        m = sm.BatchSolver(N, 2 * N, B, dtype=dtype)
+        m.setup(ops["P"], np.zeros(N), ops["A"], l, oracle.upper_bound(ops, np.zeros(4), 0.0))
+        m.mpc_set_operators(ops["Fx"], ops["Fu"], ops["Fr"], ops["Sbar"], ops["Ku"], ops["W0"])
+        Xd, Ud = torch.from_numpy(X.copy()).cuda(), torch.from_numpy(U.copy()).cuda()
+        m.mpc_step_device(Xd.data_ptr(), Ud.data_ptr(), 0.0)
+        torch.cuda.synchronize()
+        res[order] = gen + (Ud.cpu().numpy(), m.solution(), *m.info())
+    assert np.all(res["0"][2] == sm.SOLVED)
+    for k in ("1", "1b"):
+        for a, b in zip(res["0"], res[k]):
+            assert np.array_equal(a, b), k
