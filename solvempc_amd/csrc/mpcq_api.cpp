@@ -46,6 +46,7 @@ constexpr int kMaxPhases = 16;
 //   MPCQ_STREAM=graph|wave      mpcq_mpc_run_device's per-step graph or one-QP-per-wave launch
 //                               (mpcq_get_stream_path reports the choice)
 //   MPCQ_STREAM_CPW=k           plants per wave of the tile stream mode
+//   MPCQ_TAIL=wave|tile         the tile chain's last launch on the one-QP-per-wave / tile kernel
 //   MPCQ_ORDER=1                the tile path's first phase in difficulty order (mpcq_order.hip;
 //                               measured slower than index order on config 2)
 // Debug builds (-DMPCQ_DEBUG_HOOKS) add the stamp / profiling dumps (MPCQ_TILE_STAMPS,
@@ -757,33 +758,55 @@ int mpcq_warm_start(mpcq_ctx *c, const double *x, const double *y)
 }  // extern "C"
 
 // Phase boundaries of the tile path (multiples of check_termination, then max_iter): QPs still
-// running at a boundary are re-packed densely into the waves of the next launch.  One boundary at
-// 4 check_termination (100 iterations at the defaults; a second one at 3 when the batch is more than
-// ~1.5 rounds of the chip's tile-wave slots, where the re-pack at 75 pays), then one launch to
-// max_iter: the few QPs that need more than ~125 iterations finish in their (mostly idle) tile waves,
-// which beats a one-QP-per-wave launch for them (its prologue and a hand-off through HBM).
-static int phase_stops(const mpcq_settings &st, int batch, int cus, int *stops)
+// running at a boundary are re-packed densely into the waves of the next launch.  Default: stops at
+// 4 and 5 check_termination (100 and 125 iterations at the defaults), then the QPs that need more
+// (the ~tens of the long tail) finish on the one-QP-per-wave kernel: each runs on its own SIMD at
+// ~0.7 us per iteration, where a tile wave holding them runs at its slowest column's pace, ~0.9 us
+// per lone-wave iteration (config 2: 347-350 us per solve against 368-371 us for [100, max_iter] on
+// tile waves).  When the batch is more than ~1.5 rounds of the chip's tile-wave slots the
+// chain is 3, 4 check_termination and max_iter on tile waves, where the re-pack at 75 pays; a tile
+// chain forced onto a batch under 8,192 QPs (MPCQ_KERNEL=tile; the default there is the wave kernel)
+// stops at 4 check_termination and runs the rest on tile waves.
+// *wave_tail: the last launch runs on the wave kernel (test hooks MPCQ_PHASES, MPCQ_TAIL=wave|tile).
+constexpr bool kWaveTail = false;  // [100, 125] + wave tail as the default (A/B measured; parity pending)
+static int phase_stops(const mpcq_settings &st, int batch, int cus, int *stops, bool *wave_tail)
 {
     const int ct = st.check_termination;
     int np = 0;
     const char *e = test_hook("MPCQ_PHASES");  // "0" = one launch per solve, or check multiples "3,4,5"
+    const char *t = test_hook("MPCQ_TAIL");
     const bool many = (long)batch / 16 > (long)cus * 4 * 3 * 3 / 2;  // waves vs 3 waves/SIMD, 4 SIMD/CU
     int mult[kMaxPhases] = {3, 4};
     int nm = 2;
-    if (!many) {
+    *wave_tail = false;
+    if (!many && batch < 8192) {  // (a tile chain forced onto a small batch: one stop, tile waves)
         mult[0] = 4;
         nm = 1;
+    } else if (!many) {
+        mult[0] = 4;
+        mult[1] = 5;
+        *wave_tail = kWaveTail;
+        if (!kWaveTail) nm = 1;
     }
     const int cap = kMaxPhases;
     if (e[0] == '0') nm = 0;
     else if (*e) {
         nm = 0;
+        *wave_tail = false;
         for (const char *p = e; *p && nm < cap - 1;) {
             mult[nm++] = std::atoi(p);
             while (*p && *p != ',') p++;
             if (*p == ',') p++;
         }
     }
+    if (t[0] == 'w') {  // test hook: [100, 125] (or the MPCQ_PHASES list) + wave tail
+        if (!*e && !many && batch >= 8192) {
+            mult[1] = 5;
+            nm = 2;
+        }
+        *wave_tail = true;
+    }
+    if (t[0] == 't') *wave_tail = false;
     if (ct > 0) {
         for (int i = 0; i < nm; i++) {
             const long it = (long)mult[i] * ct;
@@ -793,6 +816,7 @@ static int phase_stops(const mpcq_settings &st, int batch, int cus, int *stops)
         }
     }
     stops[np++] = st.max_iter;
+    if (np < 2) *wave_tail = false;  // (phase 0 stays on tile waves)
     return np;
 }
 
@@ -813,7 +837,8 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
 {
     const int B = c->dims.batch;
     int stops[kMaxPhases];
-    const int np = phase_stops(c->set, B, c->cus, stops);
+    bool wave_tail = false;
+    const int np = phase_stops(c->set, B, c->cus, stops, &wave_tail);
     const int seg = mpcq::ListSeg::cap(B);
     const size_t lcap = (size_t)mpcq::ListSeg::kShards * seg;
     // Counter blocks: launch p zeroes block p + 1 (its successor's output) and a chain's final launch,
@@ -823,7 +848,8 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
         return -2;
     c->count0_clean = false;
     const int mpc = a.mpc;
-    const int tail_from = wave_only ? 0 : kMaxPhases;  // one QP per wave: small batches only
+    // one QP per wave: from phase 0 for small batches, else the chain's last launch (phase_stops)
+    const int tail_from = wave_only ? 0 : wave_tail ? np - 1 : kMaxPhases;
     int np_run = 0;
     a.list_seg = seg;
     // test hook: the first phase's waves take the QPs in difficulty order (mpcq_order.hip)
@@ -861,6 +887,13 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
             // one QP per wave carries no idle columns: the rest of the solve is one launch (a resumed
             // list: a multiple of ListSeg::kShards blocks)
             a.stop_iter = c->set.max_iter;
+            if (p > 0 && mpc && a.X_save) {
+                // the wave kernel reads q, u from the buffers, which a lazy phase 0 did not fill: its
+                // front end rebuilds them from X, U (the tile prologue's fp64 order) for the QPs it runs
+                a.mpc = 1;
+                a.q_out = c->d_q;
+                a.u_out = c->d_u;
+            }
             rc = wave_launch<T>(c, a, p == 0 ? B : 2048, s);
             if (rc) return rc;
             c->count0_clean = a.zero_cnt0 != nullptr;

@@ -283,12 +283,17 @@ def test_full_batch_kkt_properties(plant, dtype):
         print(f"fp32 full batch: {ties} of {B} QPs took a tie's other branch")
 
 
-def test_full_batch_mpc_step_matches_oracle(plant):
+@pytest.mark.parametrize("tail", ["default", "wave"])
+def test_full_batch_mpc_step_matches_oracle(plant, tail, monkeypatch):
     """The bench's exact path at its size: 65,536 fp32 controllerSteps through mpcq_mpc_step_device (front
     end on the device, U += x0 in the kernel) against the oracle's controllerStep on every QP: the
     applied U within F32_TOL * max(1, ||x_oracle||_inf) except at counted schedule ties, whose own
-    solution must still meet OSQP's termination criteria."""
+    solution must still meet OSQP's termination criteria.  tail=wave: the chain [100, 125] on tile
+    waves with the QPs past 125 iterations on the one-QP-per-wave kernel (MPCQ_TAIL=wave), whose
+    front end rebuilds q, u from X, U (phase 0 saved those instead of q, u)."""
     import torch
+    if tail == "wave":
+        monkeypatch.setenv("MPCQ_TAIL", "wave")
     N, B = 20, 65536
     ops, X, U, q, u = _problem(plant, N, B)
     l = np.full(2 * N, LMIN)
