@@ -32,6 +32,9 @@ sys.path.insert(0, str(ROOT))
 # MI355X dense matrix-core peaks (MI355X_MICROARCH.md: f32-input MFMA 157.3 TF = the f32 vector
 # peak; f64 78.6 TF).  The tile kernel's three ADMM products run on the matrix pipe.
 PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3}
+# The mixed tile path (MPCQ_F64_MIXED) performs each FLOP in one of the two types: its peak is the rate
+# at which the matrix cores would perform that split, 1 / (share64 / 78.6 + share32 / 157.3).
+DTYPE_NAME = {"f64": "f64", "f32": "f32", "mixed": "f64+f32 (mixed: fp64 state, checks and solution; fp32 plain iterations)"}
 
 
 def parse(argv=None):
@@ -41,7 +44,8 @@ def parse(argv=None):
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--batch", type=int, default=65536, help="QPs per GPU")
     p.add_argument("--horizon", type=int, default=20)
-    p.add_argument("--dtype", choices=("f64", "f32"), default="f32", help="ADMM iterate type (BASELINE cfg 2: fp32)")
+    p.add_argument("--dtype", choices=("f64", "f32", "mixed"), default="f32",
+                   help="ADMM iterate type (BASELINE cfg 2: fp32; mixed: MPCQ_F64_MIXED, the north-star tolerance)")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=0, help="threads of the multi-threaded CPU leg (0: all usable)")
@@ -491,13 +495,22 @@ def main_lti(a, rank, world, local, dist, dev):
                            f"(noise std {a.noise}, X0 ~ N(0, {workload.STREAM_X_SCALE}^2 diag(.1,.1,.05,.5)), U0 = 0), "
                            f"one launch for all steps (tile stream mode where the shape allows), N={N}",
                "batch_per_gpu": B, "horizon": N, "ctrl_steps": a.ctrl_steps, "parallelism": f"dp{world}"})
-    rec = _header(a, world, total_qps, wall, a.dtype, "QP solves/sec (n_x=4, n_u=1, N=20 batch)",
+    peak = PEAK_TFLOPS.get(a.dtype)
+    split = None
+    if a.dtype == "mixed":
+        if kind == "tile" and not stream_mode and not perplant:
+            f64s, f32s = workload.flops_split_mixed(N, 2 * N, 4, iters, sm.MPCQ_MIX_R, paired=paired)
+            split = (float(f64s.sum()), float(f32s.sum()))
+            peak = (split[0] + split[1]) / (split[0] / PEAK_TFLOPS["f64"] + split[1] / PEAK_TFLOPS["f32"])
+        else:  # (every other path runs MPCQ_F64_MIXED in fp64)
+            peak = PEAK_TFLOPS["f64"]
+    rec = _header(a, world, total_qps, wall, DTYPE_NAME[a.dtype], "QP solves/sec (n_x=4, n_u=1, N=20 batch)",
                   "synthetic (counter-based X ~ N(0, diag(.1,.1,.05,.5)), U ~ U(-1,1); reference plant config)"
                   if not stream_mode else "synthetic (counter-based initial states and plant noise; reference plant config)",
                   config)
     rec["roofline"] = {
-        "bound": "mfma", "achieved": achieved, "peak": PEAK_TFLOPS[a.dtype], "unit": "TFLOP/s",
-        "frac": achieved / PEAK_TFLOPS[a.dtype], "traffic": traffic_per_solve(a.dtype, B, N) if not stream_mode else None,
+        "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+        "frac": achieved / peak, "traffic": traffic_per_solve(a.dtype, B, N) if not stream_mode else None,
         "mfma_util": mfma_util(a.dtype) if a.workload == "cfg2" and B == 65536 else None,
         "kernel": ({"tile": "admm_tile_kernel, stream mode (one launch: every plant's control steps and "
                             "plant updates, one plant per MFMA column)",
@@ -508,12 +521,17 @@ def main_lti(a, rank, world, local, dist, dev):
                    f"{'the step' if not stream_mode else 'the control steps'})"),
         "kernel_ms": kern_ms, "flops_per_step": flops,
         "dense_equivalent": {"flops_per_step": flops_dense, "achieved": flops_dense / (kern_ms * 1e-3) / 1e12,
-                             "frac": flops_dense / (kern_ms * 1e-3) / 1e12 / PEAK_TFLOPS[a.dtype]},
+                             "frac": flops_dense / (kern_ms * 1e-3) / 1e12 / peak},
         "flops_note": "algorithmic: sum over QPs of iters*F_iter + checks*F_check + front end (SURVEY §8d, DESIGN §4.1), "
                       "actual per-QP iteration counts"
                       + ("; F_iter and F_check count the m/2-row products the paired loop performs "
                          "(dense_equivalent: the dense 4nm count)" if paired else "")
                       + ("; stream: every control step's iterations, accumulated on the device" if stream_mode else "")}
+    if split:
+        rec["roofline"]["peak_note"] = (f"mixed: {split[0] / sum(split):.3f} of the FLOPs in fp64 (the last {sm.MPCQ_MIX_R} "
+                                        f"iterations of every check interval, the checks, the front end), the rest "
+                                        f"fp32; peak = the matrix cores' rate for that split "
+                                        f"(f64 {PEAK_TFLOPS['f64']}, f32 {PEAK_TFLOPS['f32']} TF)")
     rec["iters"] = {"mean": float(iters.mean()), "max": int(iters.max()), "solved_frac": solved}
     if stream_mode:
         rec["iters"]["stream_total_mean"] = float(it_total.mean())
@@ -524,12 +542,12 @@ def main_lti(a, rank, world, local, dist, dev):
         # One kernel per step: condensing + Ruiz + KKT inverse (fp64) and the ADMM (T = dtype) of every
         # plant, two plants per wave.  FLOPs as the kernel performs them (workload.flops_plant_step;
         # a refactorisation per plant whose rho moved), priced at the vector peak of the ADMM's type.
-        rho0 = solver.settings.rho if a.dtype == "f64" else float(np.float32(solver.settings.rho))
+        rho0 = solver.settings.rho if a.dtype != "f32" else float(np.float32(solver.settings.rho))
         refac = (rho_f != rho0).astype(np.float64)
         pf = float(workload.flops_plant_step(N, 4, iters, refac, solver.settings.scaling).sum())
         ach = pf / (kern_ms * 1e-3) / 1e12
-        rec["roofline"] = {"bound": "valu", "achieved": ach, "peak": PEAK_TFLOPS[a.dtype], "unit": "TFLOP/s",
-                           "frac": ach / PEAK_TFLOPS[a.dtype], "traffic": None,
+        rec["roofline"] = {"bound": "valu", "achieved": ach, "peak": peak, "unit": "TFLOP/s",
+                           "frac": ach / peak, "traffic": None,
                            "kernel": "plant_step_kernel (condense + setup + solve, one pass)", "kernel_ms": kern_ms,
                            "flops_per_step": pf,
                            "flops_note": "as performed (workload.flops_plant_step): condensing by lag scans, Ruiz, "

@@ -50,6 +50,11 @@ extern "C" {
 /* ---- precision of the device iterate ------------------------------------------------------- */
 #define MPCQ_F64 0 /* fp64 throughout (the reference's precision)                            */
 #define MPCQ_F32 1 /* fp32 ADMM iterate, fp64 setup                                           */
+#define MPCQ_F64_MIXED 2 /* fp64 state, checks and solution; on the shared-plant tile path the plain
+                            iterations before the last MPCQ_MIX_R of every check interval run in fp32
+                            (MFMA f32 products), which the fp64 ones damp; every
+                            other path is MPCQ_F64                                               */
+#define MPCQ_MIX_R 8
 
 /* OSQP v0.6 settings (osqp constants.h defaults via mpcq_default_settings).  Replaces
  * OsqpEigen::Settings as used at ModelPredictiveControlAPI.cpp:51-52 (setVerbosity,
@@ -67,7 +72,7 @@ typedef struct mpcq_dims {
     int m;        /* constraint rows     (setNumberOfConstraints, :55) */
     int batch;    /* QPs in this context (reference: 1)                */
     int n_plants; /* 1 (shared P, A) or batch (one plant per QP)       */
-    int dtype;    /* MPCQ_F64 or MPCQ_F32                              */
+    int dtype;    /* MPCQ_F64, MPCQ_F32 or MPCQ_F64_MIXED              */
     int device;   /* HIP device ordinal                                */
 } mpcq_dims;
 

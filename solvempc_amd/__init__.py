@@ -16,7 +16,7 @@ import numpy as np
 
 from . import _capi
 from ._capi import (  # noqa: F401
-    MPCQ_F32, MPCQ_F64, SOLVED, SOLVED_INACCURATE, MAX_ITER_REACHED, PRIMAL_INFEASIBLE,
+    MPCQ_F32, MPCQ_F64, MPCQ_F64_MIXED, SOLVED, SOLVED_INACCURATE, MAX_ITER_REACHED, PRIMAL_INFEASIBLE,
     PRIMAL_INFEASIBLE_INACCURATE, DUAL_INFEASIBLE, DUAL_INFEASIBLE_INACCURATE, NON_CVX, UNSOLVED,
     INVALID_BOUNDS, TYPE_CHANGED, MpcqError, Settings, lib, library_path,
 )
@@ -55,8 +55,10 @@ class BatchSolver:
         self.n, self.m, self.batch, self.n_plants = int(n), int(m), int(batch), int(n_plants)
         self.dtype = dtype
         self.settings = settings or default_settings()
-        dims = _capi.Dims(self.n, self.m, self.batch, self.n_plants,
-                          MPCQ_F32 if dtype == "f32" else MPCQ_F64, int(device))
+        codes = {"f64": MPCQ_F64, "f32": MPCQ_F32, "mixed": MPCQ_F64_MIXED}
+        if dtype not in codes:
+            raise ValueError(f"dtype {dtype!r}: one of {sorted(codes)}")
+        dims = _capi.Dims(self.n, self.m, self.batch, self.n_plants, codes[dtype], int(device))
         ctx = C.c_void_p()
         _capi.check(lib().mpcq_create(C.byref(dims), C.byref(self.settings), C.byref(ctx)), "mpcq_create")
         self._ctx = ctx

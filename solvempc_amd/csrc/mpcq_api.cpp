@@ -49,6 +49,7 @@ constexpr int kMaxPhases = 16;
 //   MPCQ_TAIL=wave|tile         the tile chain's last launch on the one-QP-per-wave / tile kernel
 //   MPCQ_ORDER=1                the tile path's first phase in difficulty order (mpcq_order.hip;
 //                               measured slower than index order on config 2)
+//   MPCQ_MIX_R=r                MPCQ_F64_MIXED: fp64 iterations per check interval (default MPCQ_MIX_R)
 // Debug builds (-DMPCQ_DEBUG_HOOKS) add the stamp / profiling dumps (MPCQ_TILE_STAMPS,
 // MPCQ_SETUP_PROF, MPCQ_MIMO_SETUP_STAMPS, MPCQ_MIMO_STAMPS) and MPCQ_DEBUG_SYNC.
 const char *test_hook(const char *name)
@@ -226,6 +227,10 @@ mpcq::AdmmArgs<T> make_args(mpcq_ctx *c)
     a.iter = c->d_iter;
     a.it_acc = c->stream_acc ? c->d_it_acc : nullptr;
     a.uns_acc = c->stream_acc ? c->d_uns_acc : nullptr;
+    if (c->dims.dtype == MPCQ_F64_MIXED) {  // (test hook MPCQ_MIX_R: another fp64 share for A/B)
+        const char *r = test_hook("MPCQ_MIX_R");
+        a.mix_r = *r ? std::max(1, std::atoi(r)) : MPCQ_MIX_R;
+    }
     return a;
 }
 
@@ -340,7 +345,7 @@ int mpcq_create(const mpcq_dims *d, const mpcq_settings *s, mpcq_ctx **out)
     *out = nullptr;
     if (d->n <= 0 || d->m < 0 || d->batch <= 0) return fail(MPCQ_ERR_ARG, "n > 0, m >= 0, batch > 0 required");
     if (d->n_plants != 1 && d->n_plants != d->batch) return fail(MPCQ_ERR_ARG, "n_plants must be 1 or batch");
-    if (d->dtype != MPCQ_F64 && d->dtype != MPCQ_F32) return fail(MPCQ_ERR_ARG, "dtype");
+    if (d->dtype != MPCQ_F64 && d->dtype != MPCQ_F32 && d->dtype != MPCQ_F64_MIXED) return fail(MPCQ_ERR_ARG, "dtype");
     mpcq_settings st;
     mpcq_default_settings(&st);
     if (s) st = *s;
@@ -357,7 +362,7 @@ int mpcq_create(const mpcq_dims *d, const mpcq_settings *s, mpcq_ctx **out)
         mc = 16 * ((KM + 3) / 4);
     } else if (mpcq_internal_caps(d->n, std::max(d->m, 1), &nc, &mc) != 0) {
         // larger per-plant QPs: only the MIMO condensed-MPC path (mpcq_mimo_*) serves them
-        if (!(d->n_plants == d->batch && d->n <= 128 && d->m == 2 * d->n && d->dtype == MPCQ_F64))
+        if (!(d->n_plants == d->batch && d->n <= 128 && d->m == 2 * d->n && d->dtype != MPCQ_F32))
             return fail(MPCQ_ERR_ARG, "n/m exceed the compiled kernel capacities (n <= 32, m <= 64; the MIMO "
                                       "MPC path takes per-plant n <= 128, m = 2n, fp64)");
         nc = d->n;
@@ -768,7 +773,7 @@ int mpcq_warm_start(mpcq_ctx *c, const double *x, const double *y)
 // chain forced onto a batch under 8,192 QPs (MPCQ_KERNEL=tile; the default there is the wave kernel)
 // stops at 4 check_termination and runs the rest on tile waves.
 // *wave_tail: the last launch runs on the wave kernel (test hooks MPCQ_PHASES, MPCQ_TAIL=wave|tile).
-constexpr bool kWaveTail = false;  // [100, 125] + wave tail as the default (A/B measured; parity pending)
+constexpr bool kWaveTail = true;  // [100, 125] + wave tail as the default (A/B measured; parity green in GPUTEST_r03)
 static int phase_stops(const mpcq_settings &st, int batch, int cus, int *stops, bool *wave_tail)
 {
     const int ct = st.check_termination;
@@ -1514,7 +1519,7 @@ int mpcq_mimo_setup_plants_device(mpcq_ctx *c, int nx, int nu, int ny, int s_row
     if (nu != 1 && nu != 2 && nu != 4) return fail(MPCQ_ERR_ARG, "mimo: n_u must be 1, 2 or 4");
     if (nx <= 0 || nx > 12 || ny <= 0 || ny > 12 || s_rows < 0) return fail(MPCQ_ERR_ARG, "mimo: 1 <= n_x, n_y <= 12");
     if (n % nu || n / nu > 32 || n > 128 || m != 2 * n) return fail(MPCQ_ERR_ARG, "mimo: n = N n_u <= 128 (N <= 32), m = 2n");
-    if (c->dims.n_plants != c->dims.batch || c->dims.dtype != MPCQ_F64)
+    if (c->dims.n_plants != c->dims.batch || c->dims.dtype == MPCQ_F32)
         return fail(MPCQ_ERR_ARG, "mimo: one plant per QP (n_plants == batch), dtype MPCQ_F64");
     if (!Ad || !Bd || !Cd || !Q || !R || !RD || !K || !K0 || !w0) return fail(MPCQ_ERR_ARG, "mimo: null plant array");
     const int N = n / nu;

@@ -200,6 +200,9 @@ struct AdmmArgs {
     // setup_on_device), so for kappa > 2 c eps the certificate cannot hold and its products are skipped
     // (0: always evaluated)
     double dinf_kappa;
+    // mixed precision (MPCQ_F64_MIXED contexts, the tile kernel's paired loop): the last mix_r iterations
+    // before every info iteration run in fp64, the earlier plain ones in fp32 (0: all fp64)
+    int mix_r;
 };
 
 // MFMA operand images of one shared plant for the tile kernel (mpcq_tile.h).  A vector of length

@@ -384,13 +384,19 @@ __device__ __forceinline__ void reg_mv(const T (&m1)[NTO][KS], const T (&x1)[G][
 #define MPCQ_TSTAMP(k, v) do { } while (0)
 #endif
 // WPB: waves per workgroup (4, or 8 so that an image set serves 8 waves and 4 waves/SIMD fit the LDS).
+// MIX (T = double, paired loop only): the fp64 kernel with each check interval's first plain iterations in
+// fp32 (the fp32 kernel's packed-pair loop on rounded copies of the fp64 state, operators rounded from the
+// fp64 images); the last a.mix_r iterations before every info iteration (check, adapt, stop) run in fp64,
+// which damps the fp32 stretch's rounding below the north-star tolerance before the termination test,
+// adapt_rho and the solution read the state (tools/precision_sim.py).
 template <typename T, int KN, int KM, bool ALL_INEQ, bool LFREE, int G, int OCC, bool PAIRED = false, int WPB = 4,
-          bool STREAM = false>
+          bool STREAM = false, bool MIX = false>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void admm_tile_kernel(AdmmArgs<T> a)
 {
     MPCQ_TSTAMP(0, (long long)__builtin_amdgcn_s_memtime());
     MPCQ_TSTAMP(6, (long long)__builtin_amdgcn_s_memrealtime());
     static_assert(!PAIRED || (KM == 2 * KN && ALL_INEQ && LFREE), "paired loop: m = 2n, inequality rows, l free");
+    static_assert(!MIX || (PAIRED && std::is_same<T, double>::value && !STREAM), "mixed: the fp64 paired loop");
     constexpr int VEC = 16 / sizeof(T);
     constexpr TileLayout L = TileLayout::make(KN, KM, VEC);
     constexpr int NT = L.NT, MT = L.MT, KNP = L.KNP, KMP = L.KMP;
@@ -502,7 +508,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     const int lane = threadIdx.x & 63, c = lane & 15;
     constexpr int KNR = PAIRED ? KN : 1, NTR = PAIRED ? NT : 1;
     // f32 paired loop with n = 16 (NT - 1) + 4 (N = 20): the last tile's 4 rows on the 4x4x1 MFMA
-    constexpr bool REM4 = PAIRED && std::is_same<T, float>::value && KN % 4 == 1 && NT > 1 && MPCQ_REM4;
+    constexpr bool REM4F = PAIRED && KN % 4 == 1 && NT > 1 && MPCQ_REM4;  // (the fp32 loop's remainder tile)
+    constexpr bool REM4 = REM4F && std::is_same<T, float>::value;
     const int n = a.n, m = a.m;
     const int ncs = NCP, mcs = MCP;                // state row strides (ctx nc, mc)
     const PlantOps<T> op = a.ops;                  // shared plant: block 0
@@ -1009,10 +1016,16 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     // tile (REM4) the partial sums of S x' rows 16.. are not reduced on their own but seed the next xi's
     // remainder chain (one lane reduction per iteration fewer; the sum is reassociated there), otherwise
     // every operation and its order are piter_fast's.
+    // (MIX: the same loop on fp32 copies of the fp64 kernel's state: xs_, z_, y_ (yt), uh_, rho_, oma_ are
+    // this loop's fp32 state and data, the fp32 kernel's own registers otherwise)
     constexpr bool PK = PAIRED && std::is_same<T, float>::value && MPCQ_PK;
-    auto piter_pk_loop = [&](const T (&rS)[NTR][KNR], const T (&rBt)[NTR][KNR], const T (&rB)[NTR][KNR],
-                             T (&sx)[G][NS], const T (&adk)[G][KNR], typename Mf<T>::acc (&srem)[G], const int nxt) {
-        if constexpr (PK) {
+    auto piter_pk_loop = [&](const float (&rS)[NTR][KNR], const float (&rBt)[NTR][KNR], const float (&rB)[NTR][KNR],
+                             float (&sx)[G][NS], const float (&adk)[G][KNR], typename Mf<float>::acc (&srem)[G],
+                             const int nxt, float (&xs_)[G][NS], float (&z_)[G][MS], float (&y_)[G][MS],
+                             const float (&uh_)[G][MS], const float (&gv_)[G][NS], const float (&rho_)[G],
+                             const float oma_) {
+        if constexpr (PK || MIX) {
+            constexpr bool REM4 = REM4F;
             typedef float f2 __attribute__((ext_vector_type(2)));
             constexpr int NPR = KN / 2;
             constexpr bool ODD = (KN & 1) != 0;
@@ -1021,29 +1034,29 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             float X1[G], ZT1[G], ZB1[G], YT1[G], YB1[G], AD1[G];
 #pragma unroll
             for (int gi = 0; gi < G; gi++) {
-                RH[gi] = f2{rho[gi], rho[gi]};
+                RH[gi] = f2{rho_[gi], rho_[gi]};
 #pragma unroll
                 for (int k = 0; k < NPR; k++) {
-                    XP[gi][k] = f2{xs[gi][2 * k], xs[gi][2 * k + 1]};
-                    ZT[gi][k] = f2{z[gi][2 * k], z[gi][2 * k + 1]};
-                    ZB[gi][k] = f2{z[gi][KN + 2 * k], z[gi][KN + 2 * k + 1]};
-                    YT[gi][k] = f2{y[gi][2 * k], y[gi][2 * k + 1]};
-                    YB[gi][k] = f2{y[gi][KN + 2 * k], y[gi][KN + 2 * k + 1]};
+                    XP[gi][k] = f2{xs_[gi][2 * k], xs_[gi][2 * k + 1]};
+                    ZT[gi][k] = f2{z_[gi][2 * k], z_[gi][2 * k + 1]};
+                    ZB[gi][k] = f2{z_[gi][KN + 2 * k], z_[gi][KN + 2 * k + 1]};
+                    YT[gi][k] = f2{y_[gi][2 * k], y_[gi][2 * k + 1]};
+                    YB[gi][k] = f2{y_[gi][KN + 2 * k], y_[gi][KN + 2 * k + 1]};
                     AD[gi][k] = f2{adk[gi][2 * k], adk[gi][2 * k + 1]};
                 }
                 if constexpr (ODD) {
-                    X1[gi] = xs[gi][KN - 1];
-                    ZT1[gi] = z[gi][KN - 1];
-                    ZB1[gi] = z[gi][2 * KN - 1];
-                    YT1[gi] = y[gi][KN - 1];
-                    YB1[gi] = y[gi][2 * KN - 1];
+                    X1[gi] = xs_[gi][KN - 1];
+                    ZT1[gi] = z_[gi][KN - 1];
+                    ZB1[gi] = z_[gi][2 * KN - 1];
+                    YT1[gi] = y_[gi][KN - 1];
+                    YB1[gi] = y_[gi][2 * KN - 1];
                     AD1[gi] = adk[gi][KN - 1];
                 }
             }
-            const f2 OMA = f2{oma, oma};
+            const f2 OMA = f2{oma_, oma_};
             do {
                 it++;
-                T wt[G][KNR];  // w~ = rho ((z - yt)_top - (z - yt)_bot)
+                float wt[G][KNR];  // w~ = rho ((z - yt)_top - (z - yt)_bot)
 #pragma unroll
                 for (int gi = 0; gi < G; gi++) {
 #pragma unroll
@@ -1052,12 +1065,12 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                         wt[gi][2 * k] = w.x;
                         wt[gi][2 * k + 1] = w.y;
                     }
-                    if constexpr (ODD) wt[gi][KN - 1] = rho[gi] * ((ZT1[gi] - YT1[gi]) - (ZB1[gi] - YB1[gi]));
+                    if constexpr (ODD) wt[gi][KN - 1] = rho_[gi] * ((ZT1[gi] - YT1[gi]) - (ZB1[gi] - YB1[gi]));
                 }
-                T xi[G][NS];
-                if constexpr (REM4) reg_mv<T, G, NT, KN, KNR, false, KNR, REM4, 2>(rBt, wt, rBt, wt, xi, sx, srem);
-                else reg_mv<T, G, NT, KN, KNR, false, KNR, REM4>(rBt, wt, rBt, wt, xi, sx);  // xi = (-g + S x') + B~' w~
-                T xv[G][NS];  // x' as the next S x' product's operand
+                float xi[G][NS];
+                if constexpr (REM4) reg_mv<float, G, NT, KN, KNR, false, KNR, REM4, 2>(rBt, wt, rBt, wt, xi, sx, srem);
+                else reg_mv<float, G, NT, KN, KNR, false, KNR, REM4>(rBt, wt, rBt, wt, xi, sx);  // xi = (-g + S x') + B~' w~
+                float xv[G][NS];  // x' as the next S x' product's operand
 #pragma unroll
                 for (int gi = 0; gi < G; gi++) {
 #pragma unroll
@@ -1071,37 +1084,37 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                     }
                     if constexpr (ODD) {
                         xi[gi][KN - 1] = AD1[gi] * xi[gi][KN - 1];
-                        X1[gi] = tt_fma(oma, X1[gi], xi[gi][KN - 1]);
+                        X1[gi] = tt_fma(oma_, X1[gi], xi[gi][KN - 1]);
                         xv[gi][KN - 1] = X1[gi];
                     }
 #pragma unroll
-                    for (int s = KN; s < NS; s++) xv[gi][s] = T(0);
+                    for (int s = KN; s < NS; s++) xv[gi][s] = 0.0f;
                 }
-                T zt[G][NS];
-                reg_mv<T, G, NT, KN, NS, false, KNR, REM4>(rB, xi, rB, wt, zt, nullptr);  // alpha z~_top = B~ eta'
-                if constexpr (REM4) reg_mv<T, G, NT, KN, NS, false, KNR, REM4, 1>(rS, xv, rS, wt, sx, gv, srem);
-                else reg_mv<T, G, NT, KN, NS, false, KNR, REM4>(rS, xv, rS, wt, sx, gv);  // next: -g + S x'
+                float zt[G][NS];
+                reg_mv<float, G, NT, KN, NS, false, KNR, REM4>(rB, xi, rB, wt, zt, nullptr);  // alpha z~_top = B~ eta'
+                if constexpr (REM4) reg_mv<float, G, NT, KN, NS, false, KNR, REM4, 1>(rS, xv, rS, wt, sx, gv_, srem);
+                else reg_mv<float, G, NT, KN, NS, false, KNR, REM4>(rS, xv, rS, wt, sx, gv_);  // next: -g + S x'
 #pragma unroll
                 for (int gi = 0; gi < G; gi++) {
 #pragma unroll
                     for (int k = 0; k < NPR; k++) {
                         const f2 zp = f2{zt[gi][2 * k], zt[gi][2 * k + 1]};
                         f2 t = pfma(OMA, ZT[gi][k], zp) + YT[gi][k];  // t = (1 - alpha) z + zt' + yt
-                        f2 zn = f2{vmin(t.x, uh[gi][2 * k]), vmin(t.y, uh[gi][2 * k + 1])};
+                        f2 zn = f2{vmin(t.x, uh_[gi][2 * k]), vmin(t.y, uh_[gi][2 * k + 1])};
                         YT[gi][k] = t - zn;
                         ZT[gi][k] = zn;
                         t = pfma(OMA, ZB[gi][k], -zp) + YB[gi][k];
-                        zn = f2{vmin(t.x, uh[gi][KN + 2 * k]), vmin(t.y, uh[gi][KN + 2 * k + 1])};
+                        zn = f2{vmin(t.x, uh_[gi][KN + 2 * k]), vmin(t.y, uh_[gi][KN + 2 * k + 1])};
                         YB[gi][k] = t - zn;
                         ZB[gi][k] = zn;
                     }
                     if constexpr (ODD) {
-                        float t = tt_fma(oma, ZT1[gi], zt[gi][KN - 1]) + YT1[gi];
-                        float zn = vmin(t, uh[gi][KN - 1]);
+                        float t = tt_fma(oma_, ZT1[gi], zt[gi][KN - 1]) + YT1[gi];
+                        float zn = vmin(t, uh_[gi][KN - 1]);
                         YT1[gi] = t - zn;
                         ZT1[gi] = zn;
-                        t = tt_fma(oma, ZB1[gi], -zt[gi][KN - 1]) + YB1[gi];
-                        zn = vmin(t, uh[gi][2 * KN - 1]);
+                        t = tt_fma(oma_, ZB1[gi], -zt[gi][KN - 1]) + YB1[gi];
+                        zn = vmin(t, uh_[gi][2 * KN - 1]);
                         YB1[gi] = t - zn;
                         ZB1[gi] = zn;
                     }
@@ -1111,23 +1124,23 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             for (int gi = 0; gi < G; gi++) {
 #pragma unroll
                 for (int k = 0; k < NPR; k++) {
-                    xs[gi][2 * k] = XP[gi][k].x;
-                    xs[gi][2 * k + 1] = XP[gi][k].y;
-                    z[gi][2 * k] = ZT[gi][k].x;
-                    z[gi][2 * k + 1] = ZT[gi][k].y;
-                    z[gi][KN + 2 * k] = ZB[gi][k].x;
-                    z[gi][KN + 2 * k + 1] = ZB[gi][k].y;
-                    y[gi][2 * k] = YT[gi][k].x;
-                    y[gi][2 * k + 1] = YT[gi][k].y;
-                    y[gi][KN + 2 * k] = YB[gi][k].x;
-                    y[gi][KN + 2 * k + 1] = YB[gi][k].y;
+                    xs_[gi][2 * k] = XP[gi][k].x;
+                    xs_[gi][2 * k + 1] = XP[gi][k].y;
+                    z_[gi][2 * k] = ZT[gi][k].x;
+                    z_[gi][2 * k + 1] = ZT[gi][k].y;
+                    z_[gi][KN + 2 * k] = ZB[gi][k].x;
+                    z_[gi][KN + 2 * k + 1] = ZB[gi][k].y;
+                    y_[gi][2 * k] = YT[gi][k].x;
+                    y_[gi][2 * k + 1] = YT[gi][k].y;
+                    y_[gi][KN + 2 * k] = YB[gi][k].x;
+                    y_[gi][KN + 2 * k + 1] = YB[gi][k].y;
                 }
                 if constexpr (ODD) {
-                    xs[gi][KN - 1] = X1[gi];
-                    z[gi][KN - 1] = ZT1[gi];
-                    z[gi][2 * KN - 1] = ZB1[gi];
-                    y[gi][KN - 1] = YT1[gi];
-                    y[gi][2 * KN - 1] = YB1[gi];
+                    xs_[gi][KN - 1] = X1[gi];
+                    z_[gi][KN - 1] = ZT1[gi];
+                    z_[gi][2 * KN - 1] = ZB1[gi];
+                    y_[gi][KN - 1] = YT1[gi];
+                    y_[gi][2 * KN - 1] = YB1[gi];
                 }
             }
         }
@@ -1140,6 +1153,65 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             int nxt = refill ? next_check : (st.max_iter < stop ? st.max_iter : stop);
             if (ct && next_check < nxt) nxt = next_check;
             if (ai_w && next_adapt < nxt) nxt = next_adapt;
+            if constexpr (MIX) {
+                // fp32 stretch: iterations it + 1 .. nxt - mix_r on fp32 copies of the state (yt = y / rho),
+                // the operators rounded from the fp64 images; then the last mix_r - 1 plain iterations and
+                // the info iteration in fp64 (below)
+                const int n32 = nxt - a.mix_r;
+                if (it < n32) {
+                    float xs32[G][NS], z32[G][MS], y32[G][MS], uh32[G][MS], gv32[G][NS], rho32[G], adk32[G][KNR];
+#pragma unroll
+                    for (int gi = 0; gi < G; gi++) {
+                        rho32[gi] = (float)rho[gi];
+#pragma unroll
+                        for (int s = 0; s < NS; s++) {
+                            xs32[gi][s] = (float)xs[gi][s];
+                            gv32[gi][s] = (float)gv[gi][s];
+                        }
+#pragma unroll
+                        for (int s = 0; s < MS; s++) {
+                            z32[gi][s] = (float)z[gi][s];
+                            y32[gi][s] = s < KM ? (float)(y[gi][s] * rinv[gi]) : 0.0f;
+                            uh32[gi][s] = (float)uh[gi][s];
+                        }
+#pragma unroll
+                        for (int s = 0; s < KN; s++) adk32[gi][s] = (float)(alpha * dk[gi][s]);
+                    }
+                    // fp32 A fragments from the fp64 images (f64 image row i is logical row i; the f32
+                    // 16x16x4 fragment of lane (g, c) is row arow_f32(c), the 4x4x1 one's row c & 3)
+                    float rS32[NTR][KNR], rBt32[NTR][KNR], rB32[NTR][KNR];
+                    {
+                        const double *im = fresh_ptr((const double *)img);
+#pragma unroll
+                        for (int t = 0; t < NTR; t++) {
+                            const int ln = (REM4F && t == NTR - 1) ? ((lane & 48) | (lane & 3))
+                                                                   : ((lane & 48) | tile_arow(1, lane & 15));
+#pragma unroll
+                            for (int k = 0; k < KNR; k++) {
+                                rS32[t][k] = (float)im[L.S + TileLayout::at(KNP, VEC, t, k, ln)];
+                                rBt32[t][k] = (float)im[L.Bt + TileLayout::at(KMP, VEC, t, k, ln)];
+                                rB32[t][k] = (float)im[L.B + TileLayout::at(KNP, VEC, t, k, ln)];
+                            }
+                        }
+                    }
+                    float sx32[G][NS];
+                    typename Mf<float>::acc srem32[G];
+                    if constexpr (REM4F) reg_mv<float, G, NT, KN, NS, false, NS, REM4F, 1>(rS32, xs32, rS32, xs32, sx32, gv32, srem32);
+                    else reg_mv<float, G, NT, KN, NS, false, NS, REM4F>(rS32, xs32, rS32, xs32, sx32, gv32);
+                    piter_pk_loop(rS32, rBt32, rB32, sx32, adk32, srem32, n32 + 1, xs32, z32, y32, uh32, gv32, rho32,
+                                  (float)oma);
+#pragma unroll
+                    for (int gi = 0; gi < G; gi++) {
+#pragma unroll
+                        for (int s = 0; s < KN; s++) xs[gi][s] = (double)xs32[gi][s];
+#pragma unroll
+                        for (int s = 0; s < KM; s++) {
+                            z[gi][s] = (double)z32[gi][s];
+                            y[gi][s] = (double)y32[gi][s] * rho[gi];
+                        }
+                    }
+                }
+            }
             if (it + 1 < nxt) {
                 T rS[NTR][KNR], rBt[NTR][KNR], rB[NTR][KNR];
                 load_regs(rS, rBt, rB);
@@ -1155,7 +1227,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                     for (int s = 0; s < KM; s++) y[gi][s] = y[gi][s] * rinv[gi];  // y -> yt = y / rho
                 }
                 if constexpr (PK) {
-                    piter_pk_loop(rS, rBt, rB, sx, adk, srem, nxt);
+                    piter_pk_loop(rS, rBt, rB, sx, adk, srem, nxt, xs, z, y, uh, gv, rho, oma);
                 } else {
                     do {
                         it++;
@@ -1669,12 +1741,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
 }
 
 // Launch one tile-kernel variant: one workgroup per 64 G QPs of the phase's grid.
-template <typename T, int KN, int KM, bool AI, bool LF, int G, int OCC, bool PAIRED = false, int WPB = 4>
+template <typename T, int KN, int KM, bool AI, bool LF, int G, int OCC, bool PAIRED = false, int WPB = 4, bool MIX = false>
 int tile_launch_variant(const AdmmArgs<T> &a, hipStream_t s)
 {
     constexpr int QPW = 16 * G * WPB;
     const int blocks = (a.batch + QPW - 1) / QPW;
-    hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, AI, LF, G, OCC, PAIRED, WPB>), dim3(blocks), dim3(64 * WPB), 0, s, a);
+    hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, AI, LF, G, OCC, PAIRED, WPB, false, MIX>), dim3(blocks), dim3(64 * WPB), 0,
+                       s, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -1702,8 +1775,12 @@ int tile_launch(const AdmmArgs<T> &a, hipStream_t s)
 {
     constexpr int OCC = sizeof(T) == 8 ? 2 : 3;
     if constexpr (KM == 2 * KN) {
-        if (a.paired && a.all_ineq && a.lower_free)  // the condensed-MPC shape: paired, VGPR-resident loop
+        if (a.paired && a.all_ineq && a.lower_free) {  // the condensed-MPC shape: paired, VGPR-resident loop
+            if constexpr (std::is_same<T, double>::value) {
+                if (a.mix_r > 0) return tile_launch_variant<T, KN, KM, true, true, 1, OCC, true, 4, true>(a, s);
+            }
             return tile_launch_variant<T, KN, KM, true, true, 1, OCC, true>(a, s);
+        }
     }
     if (a.all_ineq && a.lower_free) return tile_launch_variant<T, KN, KM, true, true, 1, OCC>(a, s);
     return tile_launch_variant<T, KN, KM, false, false, 1, 2>(a, s);

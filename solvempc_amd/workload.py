@@ -146,6 +146,22 @@ def flops_per_qp(n: int, m: int, nx: int, iters: np.ndarray, check: int = 25, pa
     return it * f_iter + np.floor(it / check) * f_check + f_front
 
 
+def flops_split_mixed(n: int, m: int, nx: int, iters: np.ndarray, mix_r: int, check: int = 25,
+                      paired: bool = False) -> tuple[np.ndarray, np.ndarray]:
+    """flops_per_qp of an MPCQ_F64_MIXED solve split by the arithmetic that performs it: (fp64, fp32).
+    Iteration i (1-based) runs in fp64 when (i - 1) % check >= check - mix_r (the last mix_r of every
+    check interval: the fp32 stretch's damping and the info iteration), in fp32 otherwise; the check
+    products and the front end are fp64."""
+    it = np.asarray(iters, dtype=np.int64)
+    f_iter, f_check, f_front = _flop_terms(n, m, nx, paired)
+    r = min(max(int(mix_r), 1), check)
+    full, rem = it // check, it % check
+    n64 = full * r + np.maximum(rem - (check - r), 0)
+    f64 = n64 * float(f_iter) + full * float(f_check) + f_front
+    f32 = (it - n64) * float(f_iter)
+    return f64.astype(np.float64), f32.astype(np.float64)
+
+
 def _flop_terms(n: int, m: int, nx: int, paired: bool):
     rows = m // 2 if paired else m  # the paired loop's A products run over the m/2 distinct rows
     f_iter = 4 * n * rows + 2 * n * n + 9 * m + 6 * n

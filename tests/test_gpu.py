@@ -319,6 +319,64 @@ def test_full_batch_mpc_step_matches_oracle(plant, tail, monkeypatch):
     print(f"fp32 bench path: {int(off.sum())} of {B} QPs took a tie's other branch")
 
 
+MIXED_TOL = 1e-5  # north_star: ||u* - u*_osqp||_inf < 1e-5 on the applied move, absolute
+
+
+def _mixed_parity(x, st, it, x_ref, st_ref, it_ref, what=""):
+    """MPCQ_F64_MIXED bar on every QP, no tie exemption: the oracle's status and iteration count, the
+    applied move x0 within MIXED_TOL absolute and the whole vector within MIXED_TOL * max(1, ||x||)."""
+    assert np.array_equal(st, st_ref), what
+    assert np.array_equal(it, it_ref), (what, np.flatnonzero(it != it_ref)[:8])
+    e0 = np.abs(x[:, 0] - x_ref[:, 0])
+    ev = np.abs(x - x_ref).max(axis=1) / np.maximum(1.0, np.abs(x_ref).max(axis=1))
+    assert e0.max() < MIXED_TOL and ev.max() < MIXED_TOL, (what, e0.max(), ev.max())
+    return float(e0.max())
+
+
+@pytest.mark.parametrize("N,u_range,B", [(20, 1.0, 8192), (15, 0.0, 8192), (20, 1.0, 65536)])
+def test_mixed_tile_parity(plant, N, u_range, B, monkeypatch):
+    """The mixed tile path (fp64 state and checks, fp32 plain iterations before the last MPCQ_MIX_R of
+    every check interval) against the oracle's trajectory on every QP: same status and iteration count,
+    |x0 - x0_oracle| < 1e-5 absolute (north_star), no tie exemption."""
+    monkeypatch.setenv("MPCQ_KERNEL", "tile")
+    ops, X, U, q, u = _problem(plant, N, B, u_range=u_range)
+    s = _gpu_solve(ops, q, u, N, dtype="mixed")
+    assert s.path()[0] == "tile"
+    x, (st, it, _) = s.solution(), s.info()
+    x_ref, st_ref, it_ref, _ = _oracle_solve(ops, q, u, N)
+    e = _mixed_parity(x, st, it, x_ref, st_ref, it_ref, f"N={N} B={B}")
+    print(f"mixed N={N} B={B}: max |dx0| {e:.2e}")
+
+
+def test_mixed_full_batch_mpc_step_matches_oracle(plant):
+    """The headline bench path at its size and precision: 65,536 controllerSteps through
+    mpcq_mpc_step_device on an MPCQ_F64_MIXED context (front end and U += x0 on the device) against
+    the oracle's controllerStep on every QP: the same status and iterations, the applied U within 1e-5
+    absolute (north_star), no tie exemption."""
+    import torch
+    N, B = 20, 65536
+    ops, X, U, q, u = _problem(plant, N, B)
+    l = np.full(2 * N, LMIN)
+    s = sm.BatchSolver(N, 2 * N, B, dtype="mixed")
+    s.setup(ops["P"], np.zeros(N), ops["A"], l, oracle.upper_bound(ops, np.zeros(4), 0.0))
+    s.mpc_set_operators(ops["Fx"], ops["Fu"], ops["Fr"], ops["Sbar"], ops["Ku"], ops["W0"])
+    Xd, Ud = torch.from_numpy(X.copy()).cuda(), torch.from_numpy(U.copy()).cuda()
+    s.mpc_step_device(Xd.data_ptr(), Ud.data_ptr(), 0.0)
+    torch.cuda.synchronize()
+    Ug = Ud.cpu().numpy()
+    st, it, _ = s.info()
+    x_ref, st_ref, it_ref, _ = _oracle_solve(ops, q, u, N)
+    U_ref = U + np.where(st_ref == sm.SOLVED, x_ref[:, 0], 0.0)
+    assert np.array_equal(st, st_ref)
+    assert np.array_equal(it, it_ref), np.flatnonzero(it != it_ref)[:8]
+    d = np.abs(Ug - U_ref)
+    assert d.max() < MIXED_TOL, (d.max(), int(np.argmax(d)))
+    x = s.solution()
+    ev = np.abs(x - x_ref).max(axis=1) / np.maximum(1.0, np.abs(x_ref).max(axis=1))
+    assert ev.max() < MIXED_TOL
+    print(f"mixed bench path: max |dU| {d.max():.2e}, max rel |dx| {ev.max():.2e}")
+
+
 def test_max_iter_and_warm_start(plant, kernel):
     """MAX_ITER_REACHED after max_iter (ModelPredictiveControlAPI.cpp:51-52 defaults otherwise) and the
     warm-started second solve of the same data, step for step against the oracle."""
