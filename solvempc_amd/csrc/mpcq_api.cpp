@@ -47,8 +47,6 @@ constexpr int kMaxPhases = 16;
 //                               (mpcq_get_stream_path reports the choice)
 //   MPCQ_STREAM_CPW=k           plants per wave of the tile stream mode
 //   MPCQ_TAIL=wave|tile         the tile chain's last launch on the one-QP-per-wave / tile kernel
-//   MPCQ_ORDER=1                the tile path's first phase in difficulty order (mpcq_order.hip;
-//                               measured slower than index order on config 2)
 //   MPCQ_MIX_R=r                MPCQ_F64_MIXED: fp64 iterations per check interval (default MPCQ_MIX_R)
 // Debug builds (-DMPCQ_DEBUG_HOOKS) add the stamp / profiling dumps (MPCQ_TILE_STAMPS,
 // MPCQ_SETUP_PROF, MPCQ_MIMO_SETUP_STAMPS, MPCQ_MIMO_STAMPS) and MPCQ_DEBUG_SYNC.
@@ -139,12 +137,6 @@ struct mpcq_ctx {
     // host copies of plant-0 scaling
     std::vector<double> hD, hE;
     double hc = 1.0;
-    // difficulty order of the tile path's first phase (mpcq_order.hip): H = -A P^-1 of plant 0 (m x n)
-    // and the MPC step's key rows (m x (nx + 3)) from H and the front-end operators (host copies)
-    std::vector<double> hH, hFx, hFu, hFr1, hSbar, hKu, hW0;
-    bool order_H = false, order_K = false;
-    double *d_ordH = nullptr, *d_ordK = nullptr;
-    int *d_perm = nullptr;
 };
 
 namespace {
@@ -451,7 +443,7 @@ int mpcq_destroy(mpcq_ctx *c)
                     c->d_xs, c->d_zs, c->d_ys, c->d_rhos, c->d_snx, c->d_sny, c->d_Fx, c->d_Fu, c->d_Fr,
                     c->d_Sbar, c->d_Ku, c->d_W0, c->d_X, c->d_U, c->d_img, c->d_list, c->d_counts,
                     c->d_itstate, c->d_Ad, c->d_Bd, c->d_step, c->d_flags, c->d_stamps, c->d_mimo,
-                    c->d_it_acc, c->d_uns_acc, c->d_Xs, c->d_Us, c->d_ordH, c->d_ordK, c->d_perm};
+                    c->d_it_acc, c->d_uns_acc, c->d_Xs, c->d_Us};
     if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
     if (c->graph) (void)hipGraphDestroy(c->graph);
     for (void *p : ptrs)
@@ -580,91 +572,6 @@ int setup_on_device(mpcq_ctx *c, hipStream_t s)
     return reset_state(c, true);
 }
 
-// The MPC step's key rows K [m][nx + 3] (mpcq_order.hip) from H and the front-end operators.
-static int build_order_K(mpcq_ctx *c)
-{
-    c->order_K = false;
-    if (!c->order_H || !c->mpc_ready || c->hFx.empty()) return MPCQ_OK;
-    const int n = c->dims.n, m = c->dims.m, nx = c->nx, w = nx + 3;
-    std::vector<double> K((size_t)m * w);
-    for (int j = 0; j < m; j++) {
-        const double *h = &c->hH[(size_t)j * n];
-        for (int t = 0; t < nx; t++) {
-            double s = -c->hSbar[(size_t)j * nx + t];
-            for (int v = 0; v < n; v++) s += h[v] * c->hFx[(size_t)v * nx + t];
-            K[(size_t)j * w + t] = s;
-        }
-        double su = -c->hKu[j], sr = 0.0;
-        for (int v = 0; v < n; v++) {
-            su += h[v] * c->hFu[v];
-            sr += h[v] * c->hFr1[v];
-        }
-        K[(size_t)j * w + nx] = su;
-        K[(size_t)j * w + nx + 1] = sr;
-        K[(size_t)j * w + nx + 2] = -c->hW0[j];
-    }
-    if (c->d_ordK) (void)hipFree(c->d_ordK);
-    c->d_ordK = nullptr;
-    c->gen++;
-    if (hipMalloc((void **)&c->d_ordK, 8 * K.size()) != hipSuccess) return fail(MPCQ_ERR_HIP, "hipMalloc failed");
-    int rc = h2d(c->d_ordK, K.data(), 8 * K.size(), c->last);
-    if (rc) return rc;
-    HIPCHK(hipStreamSynchronize(c->last));  // (K is a local)
-    c->order_K = true;
-    return MPCQ_OK;
-}
-
-// H = -A P^-1 of a shared plant (Gauss-Jordan with partial pivoting on P, fp64) and the order buffers.
-// A plant whose P does not invert cleanly is not ordered (the batch keeps its index order).
-static int build_order_H(mpcq_ctx *c, const double *P, const double *A)
-{
-    c->order_H = c->order_K = false;
-    const int n = c->dims.n, m = c->dims.m;
-    const size_t B = c->dims.batch;
-    if (c->dims.n_plants != 1 || n > 32 || m > 64 || m == 0) return MPCQ_OK;
-    // [P | A'] -> [I | P^-1 A']
-    const int w = n + m;
-    std::vector<double> T((size_t)n * w);
-    for (int i = 0; i < n; i++) {
-        for (int k = 0; k < n; k++) T[(size_t)i * w + k] = P[(size_t)i * n + k];
-        for (int j = 0; j < m; j++) T[(size_t)i * w + n + j] = A[(size_t)j * n + i];
-    }
-    double pmax = 0.0;
-    for (int i = 0; i < n * n; i++) pmax = std::max(pmax, std::fabs(P[i]));
-    for (int col = 0; col < n; col++) {
-        int piv = col;
-        for (int i = col + 1; i < n; i++)
-            if (std::fabs(T[(size_t)i * w + col]) > std::fabs(T[(size_t)piv * w + col])) piv = i;
-        const double d = T[(size_t)piv * w + col];
-        if (!(std::fabs(d) > 1e-12 * pmax)) return MPCQ_OK;
-        if (piv != col)
-            for (int k = 0; k < w; k++) std::swap(T[(size_t)piv * w + k], T[(size_t)col * w + k]);
-        for (int k = 0; k < w; k++) T[(size_t)col * w + k] /= d;
-        for (int i = 0; i < n; i++) {
-            const double f = T[(size_t)i * w + col];
-            if (i == col || f == 0.0) continue;
-            for (int k = 0; k < w; k++) T[(size_t)i * w + k] -= f * T[(size_t)col * w + k];
-        }
-    }
-    c->hH.assign((size_t)m * n, 0.0);
-    for (int j = 0; j < m; j++)
-        for (int i = 0; i < n; i++) {
-            const double v = -T[(size_t)i * w + n + j];  // (P^-1 A')' = A P^-1 (P symmetric)
-            if (!std::isfinite(v)) return MPCQ_OK;
-            c->hH[(size_t)j * n + i] = v;
-        }
-    if (!c->d_ordH) {
-        if (hipMalloc((void **)&c->d_ordH, 8 * (size_t)64 * 32) != hipSuccess ||
-            hipMalloc((void **)&c->d_perm, 4 * std::max<size_t>(B, 1)) != hipSuccess)
-            return fail(MPCQ_ERR_HIP, "hipMalloc failed");
-    }
-    int rc = h2d(c->d_ordH, c->hH.data(), 8 * c->hH.size(), c->last);
-    if (rc) return rc;
-    HIPCHK(hipStreamSynchronize(c->last));
-    c->order_H = true;
-    return build_order_K(c);
-}
-
 int mpcq_setup(mpcq_ctx *c, const double *P, const double *q0, const double *A, const double *l0,
                const double *u0)
 {
@@ -686,7 +593,6 @@ int mpcq_setup(mpcq_ctx *c, const double *P, const double *q0, const double *A, 
         (rc = h2d(c->d_u0, u0, 8 * Pn * m, s)))
         return rc;
     if ((rc = setup_on_device(c, s))) return rc;
-    if ((rc = build_order_H(c, P, A))) return rc;
     c->lower_free = lower_all_free(c, l0);
     c->gen++;
     c->mode = mpcq_ctx::Mode::Generic;
@@ -857,14 +763,6 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
     const int tail_from = wave_only ? 0 : wave_tail ? np - 1 : kMaxPhases;
     int np_run = 0;
     a.list_seg = seg;
-    // test hook: the first phase's waves take the QPs in difficulty order (mpcq_order.hip)
-    const int *perm = nullptr;
-    if (!wave_only && (mpc ? c->order_K : c->order_H) && test_hook("MPCQ_ORDER")[0] == '1') {
-        if (mpcq_internal_order(B, c->dims.n, c->dims.m, c->nx, c->d_ordK, c->d_ordH, mpc ? a.X : nullptr, a.U,
-                                a.xref, a.q, a.u, c->d_perm, s) != 0)
-            return -2;
-        perm = c->d_perm;
-    }
 
     // debug build: per-wave stage stamps of every phase launch, written to $MPCQ_TILE_STAMPS after the solve
     const char *stp = debug_hook("MPCQ_TILE_STAMPS");
@@ -883,7 +781,6 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
         a.stop_iter = stops[p];
         a.resume = p > 0;
         a.mpc = p == 0 ? mpc : 0;  // later phases read q, u from the buffers phase 0 filled
-        a.perm = p == 0 ? perm : nullptr;
         const bool final_launch = p + 1 == np || (p >= tail_from && c->dims.n <= 32 && c->dims.m <= 64);
         a.zero_cnt = final_launch ? nullptr : c->d_counts + (size_t)(p + 1) * mpcq::ListSeg::kCounters;
         a.zero_cnt0 = (final_launch && p >= 2) ? c->d_counts : nullptr;
@@ -1138,17 +1035,6 @@ int mpcq_mpc_set_operators(mpcq_ctx *c, int nx, const double *Fx, const double *
         (rc = h2d(c->d_Ku, Ku, 8 * Pn * m, s)) || (rc = h2d(c->d_W0, W0, 8 * Pn * m, s)))
         return rc;
     c->mpc_ready = true;
-    if (Pn == 1) {  // host copies for the difficulty order's key rows
-        c->hFx.assign(Fx, Fx + n * nx);
-        c->hFu.assign(Fu, Fu + n);
-        c->hFr1.assign(n, 0.0);
-        for (size_t v = 0; v < n; v++)
-            for (size_t t = 0; t < n; t++) c->hFr1[v] += Fr[v * n + t];
-        c->hSbar.assign(Sbar, Sbar + m * nx);
-        c->hKu.assign(Ku, Ku + m);
-        c->hW0.assign(W0, W0 + m);
-        return build_order_K(c);
-    }
     return MPCQ_OK;
 }
 
@@ -1472,7 +1358,6 @@ int mpcq_mpc_setup_plants_device(mpcq_ctx *c, int nx, int s_rows, const double *
     c->lower_free = true;  // l0 = -DBL_MAX on every row (:42)
     c->gen++;
     c->mpc_ready = true;
-    c->order_H = c->order_K = false;  // (operators built on the device: no host H, index order)
     c->mode = mpcq_ctx::Mode::Generic;
     return MPCQ_OK;
 }

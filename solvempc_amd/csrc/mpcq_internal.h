@@ -190,7 +190,6 @@ struct AdmmArgs {
     int list_seg;               // ListSeg segment capacity
     int *it_state;              // [batch] iterations done so far in this solve
     int qp0;                    // QP index of identity-list slot 0 (sub-batch parts of a tile solve)
-    const int *perm;            // first phase: slot -> QP (mpcq_order.hip difficulty order; null: identity)
     int stop_iter;              // phase boundary (multiple of check_termination, or max_iter)
     int resume;                 // 1: phase >= 2 (state, rho and iteration count come from the buffers)
     long long *stamps;          // debug build (MPCQ_DEBUG_HOOKS): [wave][8] s_memtime stamps, or null
@@ -377,11 +376,6 @@ int mpcq_internal_front_end(int batch, int nx, int n, int m, const double *Xs, c
                             const double *Fx, const double *Fu, const double *Fr, const double *Sbar,
                             const double *Ku, const double *W0, double *q, double *u, hipStream_t s);
 int mpcq_internal_set_step(long long *step, long long v, hipStream_t s);
-// Difficulty order of a shared-plant batch (mpcq_order.hip): perm = each 1024-QP window's QPs by
-// descending key bin.  MPC step when X is non-null (key rows K [m][nx + 3]), else the generic q, u with
-// H [m][n].  0 launched, -1 unsupported shape.
-int mpcq_internal_order(int batch, int n, int m, int nx, const double *K, const double *H, const double *X,
-                        const double *U, double xref, const double *q, const double *u, int *perm, hipStream_t s);
 // MIMO condensed MPC (mpcq_mimo.hip): per-plant condensing + Ruiz + P^, then the per-QP solve
 // (one 512-thread workgroup per QP: KKT inverse by Gauss-Jordan in VGPRs, structured A).
 int mpcq_internal_mimo_setup_launch(const mpcq::MimoSetupArgs *a, hipStream_t s);

@@ -416,6 +416,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? M
     const double rho0 = fmin(fmax(st.rho, kRhoMin), kRhoMax);
     T xs = T(0), zt = T(0), zb = T(0), yt = T(0), yb = T(0);
     T rho = (T)rho0, rinv = T(1) / rho;
+    // the rho this half's M(rho)^-1 is built at: rho0 until adapt_rho moves it (an fp32 half keeps the
+    // fp64 rho0, not (double)(float)rho0, so a rebuild its partner half triggers reproduces its bits)
+    double rho_f = rho0;
     const T alpha = (T)st.alpha, oma = T(1) - (T)st.alpha;
     const T ET = (T)(lr ? Er : 0.0), DT = (T)Dd, K0T = (T)K0;
     const T EK = ET * K0T;  // (A^ x)_r = E_r K0 sum_{k<=r} D_k x_k
@@ -462,8 +465,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? M
 
     for (;;) {
         if (refactor) {  // initSolver's factorisation, then OSQP's refactorisation after a rho change (each
-                         // half at its own rho; a half whose rho did not move rebuilds the same bits)
-            const bool ok = factor(first ? rho0 : (double)rho);
+                         // half at its own rho_f; a half whose rho did not move rebuilds the same bits)
+            const bool ok = factor(rho_f);
             refactor = false;
             if (first) {
                 first = false;
@@ -618,6 +621,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? M
             if (!done && (rn > rhod * st.adaptive_rho_tolerance || rn < rhod / st.adaptive_rho_tolerance)) {
                 rho = (T)rn;
                 rinv = T(1) / rho;
+                rho_f = (double)rho;
                 refactor = true;
             }
         }

@@ -1732,7 +1732,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             const int slot = wave_slot + 16 * gi + c;
             valid[gi] = slot < count && (!refill || c < cpw);
             const int i = slot + (seglist ? seg * a.list_seg : 0);  // list entry
-            b_[gi] = valid[gi] ? (seglist ? a.list_in[i] : a.perm ? a.perm[a.qp0 + i] : a.qp0 + i) : 0;
+            b_[gi] = valid[gi] ? (seglist ? a.list_in[i] : a.qp0 + i) : 0;
         }
         run_group(b_, valid);
     }

@@ -1058,30 +1058,29 @@ def test_formulations_do_not_mix(plant):
     assert np.all(s.info()[0] == sm.SOLVED)
 
 
-@pytest.mark.parametrize("dtype", ["f32", "f64"])
-def test_difficulty_order_is_bit_identical(plant, dtype, monkeypatch):
-    """With MPCQ_ORDER=1 the tile path's first phase takes the QPs in difficulty order (mpcq_order.hip):
-    only the wave a QP runs in changes, so the generic solve and the controllerStep path give
-    bit-identical solutions, duals, statuses and iteration counts in index and difficulty order, and
-    two ordered solves agree bit for bit although the order inside a bin is set by atomics.  (This is
-    also the check that a QP's arithmetic does not depend on the other columns of its wave.)"""
+@pytest.mark.parametrize("dtype", ["f32", "f64", "mixed"])
+def test_results_independent_of_batch_order(plant, dtype, monkeypatch):
+    """A QP's arithmetic does not depend on the wave or the other columns it runs with: the batch in
+    index order and the same QPs in a random permutation give bit-identical solutions, duals,
+    statuses and iteration counts on the tile path (generic solve and the controllerStep path)."""
     import torch
     N, B = 20, 16384
     ops, X, U, q, u = _problem(plant, N, B, seed=31)
     l = np.full(2 * N, LMIN)
-    res = {}
-    for order in ("0", "1", "1b"):
-        monkeypatch.setenv("MPCQ_ORDER", order[0])
-        s = _gpu_solve(ops, q, u, N, dtype=dtype)
+    perm = np.random.default_rng(7).permutation(B)
+    res = []
+    for p in (np.arange(B), perm):
+        s = _gpu_solve(ops, q[p], u[p], N, dtype=dtype)
+        assert s.path()[0] == "tile"
         gen = (s.solution(), s.dual(), *s.info())
         m = sm.BatchSolver(N, 2 * N, B, dtype=dtype)
         m.setup(ops["P"], np.zeros(N), ops["A"], l, oracle.upper_bound(ops, np.zeros(4), 0.0))
         m.mpc_set_operators(ops["Fx"], ops["Fu"], ops["Fr"], ops["Sbar"], ops["Ku"], ops["W0"])
-        Xd, Ud = torch.from_numpy(X.copy()).cuda(), torch.from_numpy(U.copy()).cuda()
+        Xd, Ud = torch.from_numpy(X[p].copy()).cuda(), torch.from_numpy(U[p].copy()).cuda()
         m.mpc_step_device(Xd.data_ptr(), Ud.data_ptr(), 0.0)
         torch.cuda.synchronize()
-        res[order] = gen + (Ud.cpu().numpy(), m.solution(), *m.info())
-    assert np.all(res["0"][2] == sm.SOLVED)
-    for k in ("1", "1b"):
-        for a, b in zip(res["0"], res[k]):
-            assert np.array_equal(a, b), k
+        inv = np.argsort(p)
+        res.append([v[inv] for v in gen + (Ud.cpu().numpy(), m.solution(), *m.info())])
+    assert np.all(res[0][2] == sm.SOLVED)
+    for a, b in zip(res[0], res[1]):
+        assert np.array_equal(a, b)
