@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -304,6 +305,8 @@ int h2d(void *dst, const void *src, size_t bytes, hipStream_t s)
 
 }  // namespace
 
+static void verbose_header(const mpcq_ctx *c, const char *what);  // (settings.verbose: below)
+
 extern "C" {
 
 void mpcq_default_settings(mpcq_settings *s)
@@ -596,6 +599,7 @@ int mpcq_setup(mpcq_ctx *c, const double *P, const double *q0, const double *A, 
     c->lower_free = lower_all_free(c, l0);
     c->gen++;
     c->mode = mpcq_ctx::Mode::Generic;
+    verbose_header(c, "mpcq_setup (osqp_setup: Ruiz scaling, constraint types, KKT basis)");
     return MPCQ_OK;
 }
 
@@ -881,15 +885,132 @@ static int launch_typed(mpcq_ctx *c, hipStream_t s, bool mpc, const double *X, d
     return launch_args<T>(c, a, s);
 }
 
+// ---- settings.verbose (osqp-eigen setVerbosity, ModelPredictiveControlAPI.cpp:51, solver.cpp:21-25):
+// OSQP v0.6's setup header, its iteration summary line and its status footer, for QP 0 of the context
+// (the reference's one QP), plus the batch's status counts.  The device keeps no per-iteration record,
+// so the summary is the final iterate's line: objective, primal and dual residual of the returned
+// (x, y) in the unscaled problem, the final rho, the host-timed solve.  Printed on stdout as OSQP does;
+// a verbose solve synchronises its stream.
+static const char *status_name(int st)
+{
+    switch (st) {
+    case MPCQ_SOLVED: return "solved";
+    case MPCQ_SOLVED_INACCURATE: return "solved inaccurate";
+    case MPCQ_MAX_ITER_REACHED: return "maximum iterations reached";
+    case MPCQ_PRIMAL_INFEASIBLE: return "primal infeasible";
+    case MPCQ_DUAL_INFEASIBLE: return "dual infeasible";
+    case MPCQ_NON_CVX: return "problem non convex";
+    case MPCQ_INVALID_BOUNDS: return "invalid bounds (u < l)";
+    case MPCQ_TYPE_CHANGED: return "constraint type changed (re-run setup)";
+    case MPCQ_UNSOLVED: return "unsolved";
+    default: return st == 3 ? "primal infeasible inaccurate" : st == 4 ? "dual infeasible inaccurate" : "unknown";
+    }
+}
+
+static void verbose_header(const mpcq_ctx *c, const char *what)
+{
+    if (!c->set.verbose) return;
+    const mpcq_settings &s = c->set;
+    const char *dt = c->dims.dtype == MPCQ_F32 ? "fp32 iterate, fp64 setup"
+                     : c->dims.dtype == MPCQ_F64_MIXED ? "fp64 (fp32 plain iterations on the tile path)" : "fp64";
+    std::printf("-----------------------------------------------------------------\n"
+                "   libmpcq: batched OSQP-v0.6 ADMM on gfx950 (solvempc_amd)\n"
+                "-----------------------------------------------------------------\n");
+    std::printf("problem:  variables n = %d, constraints m = %d\n", c->dims.n, c->dims.m);
+    std::printf("          batch = %d QPs, %s, %s\n", c->dims.batch,
+                c->dims.n_plants == 1 ? "one shared (P, A)" : "one (P, A) per QP", dt);
+    std::printf("          setup: %s\n", what);
+    std::printf("settings: linear system solver = reduced KKT on the device (%s),\n",
+                c->tile ? "eigenbasis, MFMA tile kernel" : c->inv_ops ? "direct inverse" : "eigenbasis");
+    std::printf("          eps_abs = %.1e, eps_rel = %.1e,\n", s.eps_abs, s.eps_rel);
+    std::printf("          eps_prim_inf = %.1e, eps_dual_inf = %.1e,\n", s.eps_prim_inf, s.eps_dual_inf);
+    std::printf("          rho = %.2e %s,\n", s.rho, s.adaptive_rho ? "(adaptive)" : "");
+    std::printf("          sigma = %.2e, alpha = %.2f, max_iter = %d\n", s.sigma, s.alpha, s.max_iter);
+    if (s.check_termination) std::printf("          check_termination: on (interval %d),\n", s.check_termination);
+    else std::printf("          check_termination: off,\n");
+    std::printf("          scaling: %s, scaled_termination: %s\n", s.scaling ? "on" : "off",
+                s.scaled_termination ? "on" : "off");
+    std::printf("          warm start: %s, polish: off, time_limit: off\n\n", s.warm_start ? "on" : "off");
+    std::fflush(stdout);
+}
+
+static void verbose_solve(mpcq_ctx *c, double seconds)
+{
+    const size_t B = c->dims.batch, n = c->dims.n, m = c->dims.m;
+    std::vector<int> st(B), it(B);
+    std::vector<double> rho(B), x(n), y(m), q(n), u(m), l(m), P(n * n), A(m * n);
+    if (hipStreamSynchronize(c->last) != hipSuccess ||
+        hipMemcpy(st.data(), c->d_status, 4 * B, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(it.data(), c->d_iter, 4 * B, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(rho.data(), c->d_rho, 8 * B, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(x.data(), c->d_x, 8 * n, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(y.data(), c->d_y, 8 * m, hipMemcpyDeviceToHost) != hipSuccess)
+        return;
+    // QP 0's data in the unscaled problem (generic contexts: plant 0's P, A and this solve's q, l, u)
+    bool have = c->mode == mpcq_ctx::Mode::Generic && materialize_qu(c) == MPCQ_OK &&
+                hipMemcpy(q.data(), c->d_q, 8 * n, hipMemcpyDeviceToHost) == hipSuccess &&
+                hipMemcpy(u.data(), c->d_u, 8 * m, hipMemcpyDeviceToHost) == hipSuccess &&
+                hipMemcpy(l.data(), c->d_l, 8 * m, hipMemcpyDeviceToHost) == hipSuccess &&
+                hipMemcpy(P.data(), c->d_P, 8 * n * n, hipMemcpyDeviceToHost) == hipSuccess &&
+                hipMemcpy(A.data(), c->d_A, 8 * m * n, hipMemcpyDeviceToHost) == hipSuccess;
+    const bool sol = st[0] == MPCQ_SOLVED || st[0] == MPCQ_SOLVED_INACCURATE || st[0] == MPCQ_MAX_ITER_REACHED;
+    double obj = 0.0, pri = 0.0, dua = 0.0;
+    if (have && sol) {
+        std::vector<double> Px(n, 0.0), Aty(n, 0.0);
+        for (size_t i = 0; i < n; i++)
+            for (size_t k = 0; k < n; k++) Px[i] += P[std::min(i, k) * n + std::max(i, k)] * x[k];  // upper triangle
+        for (size_t j = 0; j < m; j++) {
+            double ax = 0.0;
+            for (size_t k = 0; k < n; k++) {
+                ax += A[j * n + k] * x[k];
+                Aty[k] += A[j * n + k] * y[j];
+            }
+            pri = std::max(pri, std::max(ax - u[j], l[j] - ax));
+        }
+        for (size_t i = 0; i < n; i++) {
+            obj += 0.5 * x[i] * Px[i] + q[i] * x[i];
+            dua = std::max(dua, std::fabs(Px[i] + q[i] + Aty[i]));
+        }
+    }
+    std::printf("iter   objective    pri res    dua res    rho        time\n");
+    if (have && sol) std::printf("%4d  %12.4e  %9.2e  %9.2e  %9.2e  %9.2es\n\n", it[0], obj, pri, dua, rho[0], seconds);
+    else std::printf("%4d  %12s  %9s  %9s  %9.2e  %9.2es\n\n", it[0], "-", "-", "-", rho[0], seconds);
+    std::printf("status:               %s\n", status_name(st[0]));
+    std::printf("number of iterations: %d\n", it[0]);
+    if (have && sol) std::printf("optimal objective:    %.4f\n", obj);
+    std::printf("run time:             %.2es\n", seconds);
+    std::printf("final rho:            %.2e\n", rho[0]);
+    if (B > 1) {
+        size_t solved = 0;
+        long long tot = 0;
+        int mn = it[0], mx = it[0];
+        for (size_t b = 0; b < B; b++) {
+            solved += st[b] == MPCQ_SOLVED;
+            tot += it[b];
+            mn = std::min(mn, it[b]);
+            mx = std::max(mx, it[b]);
+        }
+        std::printf("batch:                %zu QPs, %zu solved, iterations %d / %.1f / %d (min / mean / max)\n", B,
+                    solved, mn, (double)tot / B, mx);
+    }
+    std::printf("\n");
+    std::fflush(stdout);
+}
+
 extern "C" {
 
 static int launch_solve(mpcq_ctx *c, hipStream_t s, bool mpc, const double *X, double *U, double xref)
 {
+    const auto t0 = std::chrono::steady_clock::now();
     const int rc = c->dims.dtype == MPCQ_F32 ? launch_typed<float>(c, s, mpc, X, U, xref)
                                              : launch_typed<double>(c, s, mpc, X, U, xref);
     if (rc) return fail(MPCQ_ERR_HIP, std::string("ADMM kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
     c->last = s;
     c->fresh = false;
+    if (c->set.verbose) {
+        (void)hipStreamSynchronize(s);
+        verbose_solve(c, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+    }
     return MPCQ_OK;
 }
 
@@ -1359,6 +1480,7 @@ int mpcq_mpc_setup_plants_device(mpcq_ctx *c, int nx, int s_rows, const double *
     c->gen++;
     c->mpc_ready = true;
     c->mode = mpcq_ctx::Mode::Generic;
+    verbose_header(c, "mpcq_mpc_setup_plants_device (condensing + osqp_setup per plant)");
     return MPCQ_OK;
 }
 

@@ -46,7 +46,7 @@ def _oracle_wire(lines, plant):
     l = np.full(2 * N, LMIN)
     r = oracle.Solver(ops["P"], oracle.gradient(ops, np.zeros(4), 0.0, xref), ops["A"], l,
                       oracle.upper_bound(ops, np.zeros(4), 0.0))
-    U, out = 0.0, []
+    U, out, iters = 0.0, [], []
     for line in lines:
         if len(line) + 1 > 30:  # readPort: num_bytes > 30
             tok = line.split()
@@ -55,7 +55,9 @@ def _oracle_wire(lines, plant):
             assert r.update_upper_bound(oracle.upper_bound(ops, X, U))
             assert r.solve() == oracle.SOLVED
             U += r.x()[0]
+            iters.append(r.info().iter)
         out.append(("%f" % U)[:8])  # std::to_string(U), first sizeof(char*) bytes
+    _oracle_wire.iters = iters
     return out
 
 
@@ -82,6 +84,18 @@ def test_cli_replay_matches_oracle_controller(tmp_path, plant):
     np.testing.assert_allclose(H, P, rtol=1e-5, atol=1e-9)
     for name in ("Ad", "Bd", "Sx", "Su", "Sbar", "LL", "Fu", "Fr", "Fx", "Gbar", "Qbar"):
         assert f"\n{name}:\n" in log, name
+    # -v also turns on the solver's own output (ModelPredictiveControlAPI.cpp:51 setVerbosity): the
+    # setup header once, then per controllerStep the final iterate's summary line and the status block,
+    # whose iteration counts are the oracle's
+    assert log.count("libmpcq: batched OSQP-v0.6 ADMM on gfx950") == 1
+    assert "eps_abs = 1.0e-03, eps_rel = 1.0e-03," in log and "warm start: on, polish: off" in log
+    steps = sum(len(x) + 1 > 30 for x in lines)
+    assert log.count("status:               solved\n") == steps
+    its = [int(v) for v in re.findall(r"number of iterations: (\d+)", log)]
+    assert its == _oracle_wire.iters
+    for row in re.findall(r"iter   objective    pri res    dua res    rho        time\n(.*)\n", log):
+        it, obj, pri, dua, rho, t = row.split()
+        assert float(pri) <= 1e-3 * 10 and float(dua) <= 1e-3 * 10 and t.endswith("s")
 
 
 def test_reference_shaped_eigen_caller_on_device(tmp_path, plant):
