@@ -55,6 +55,11 @@ def parse(argv=None):
                         "(randomised plants, per-GPU shard of 1M: condense + setup + one controllerStep each); "
                         "quadrotor: config 4 (262,144 quad-rotor hover linearisations, n_x 12, n_u 4, N 30: MIMO "
                         "condense + setup + one controllerStep each, fp64)")
+    p.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                   help="weak: --batch QPs per GPU; strong: one global batch (--global-batch) split over the GPUs "
+                        "(dist.strong_block); BASELINE config 3 is `--workload perplant --scaling strong`")
+    p.add_argument("--global-batch", type=int, default=0,
+                   help="strong scaling: QPs of the whole job (default: 1,048,576 for perplant, else --batch)")
     p.add_argument("--ctrl-steps", type=int, default=1000, help="control steps per bench step (stream)")
     p.add_argument("--noise", type=float, default=1e-2, help="plant noise std (stream; SURVEY §8d: var 1e-4)")
     p.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
@@ -66,6 +71,8 @@ def parse(argv=None):
         a.batch = 4096
     if a.workload == "perplant" and a.batch == 65536:
         a.batch = 131072  # 1,048,576 / 8 GPUs
+    if a.scaling == "strong" and not a.global_batch:
+        a.global_batch = 1 << 20 if a.workload == "perplant" else a.batch  # BASELINE config 3: 1,048,576 plants
         if a.seed == 1:
             a.seed = 2  # SURVEY §8d config 3 seed
     if a.workload == "stream" and a.seed == 1:
@@ -92,6 +99,8 @@ def launch_ranks(a, argv) -> int:
     """One process per GPU, started before anything in this process touches a GPU.  Each child gets
     torch.distributed.run's environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT);
     rank 0's JSON line is relayed.  Returns the worst child exit code."""
+    import threading
+
     port = _free_port()
     procs = []
     for r in range(a.gpus):
@@ -99,11 +108,29 @@ def launch_ranks(a, argv) -> int:
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + argv, env=env,
                                       stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
-    out, _ = procs[0].communicate()
-    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
-    sys.stdout.write(out)
+    out = []
+    reader = threading.Thread(target=lambda: out.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    # poll every rank: the first one to fail ends the others (they would otherwise wait in the rendezvous
+    # or the gather until the backend's timeout)
+    while any(p.poll() is None for p in procs):
+        if any(p.poll() not in (None, 0) for p in procs):
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            break
+        time.sleep(0.05)
+    reader.join(timeout=30)
+    rcs = [p.wait() for p in procs]
+    sys.stdout.write(out[0] if out else "")
     sys.stdout.flush()
-    return max(rcs, key=abs)
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
 
 
 def world_from_env(a):
@@ -272,7 +299,21 @@ def main_quadrotor(a, rank, world, local, dist, dev):
 def _header(a, world, value, wall, dtype, metric, data, config):
     return {"metric": metric, "value": value, "unit": "QP/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": wall / a.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": data, "config": config}
+            "scaling": getattr(a, "scaling", "weak"), "vs_baseline": None, "dtype": dtype, "data": data,
+            "config": config}
+
+
+def blocks(a, rank, world):
+    """This rank's block of the global counter-based stream: (start, count, padded length, QPs of the job).
+    weak: --batch per rank; strong: --global-batch split into near-equal contiguous blocks, each rank's
+    moves padded to the longest block for the equal-size gather."""
+    from solvempc_amd import dist as mdist
+
+    if a.scaling == "strong":
+        start, count = mdist.strong_block(a.global_batch, rank, world)
+        return start, count, -(-a.global_batch // world), a.global_batch
+    start, count = mdist.weak_block(a.batch, rank)
+    return start, count, count, a.batch * world
 
 
 def _collective(dist, world, got):
@@ -345,9 +386,10 @@ def main_dry(a, rank, world, dist):
     from solvempc_amd import dist as mdist
     from solvempc_amd import workload
 
-    start, count = mdist.weak_block(a.batch, rank)
+    start, count, pad, total = blocks(a, rank, world)
     _, U = workload.mpc_states(a.seed, start, count)
-    U_t = torch.from_numpy(U)
+    U_t = torch.zeros(pad, dtype=torch.float64)
+    U_t[:count] = torch.from_numpy(U)
     gathered = [torch.empty_like(U_t) for _ in range(world)] if rank == 0 else None
     wall, got = _timed_loop(a, lambda i=None: mdist.gather_moves(dist, U_t, world, rank, gathered), dist, world,
                             torch.device("cpu"))
@@ -355,11 +397,14 @@ def main_dry(a, rank, world, dist):
         return None
     rec = _header(a, world, None, wall, a.dtype, "QP solves/sec (n_x=4, n_u=1, N=20 batch)",
                   "dry run: no device, no solve", {"workload": "dry run of the launcher and the gather",
-                                                    "batch_per_gpu": a.batch, "parallelism": f"dp{world}"})
+                                                    "batch_per_gpu": count, "global_batch": total,
+                                                    "parallelism": f"dp{world}"})
     rec["dry_run"] = True
     rec["collective"] = _collective(dist, world, got)
-    full = torch.cat(got).numpy()
-    rec["collective"]["matches_stream"] = bool(np.array_equal(full, workload.mpc_states(a.seed, 0, a.batch * world)[1]))
+    full = np.concatenate([t.numpy()[:mdist.strong_block(total, r, world)[1] if a.scaling == "strong" else count]
+                           for r, t in enumerate(got)])
+    rec["collective"]["gathered"] = int(full.size)
+    rec["collective"]["matches_stream"] = bool(np.array_equal(full, workload.mpc_states(a.seed, 0, total)[1]))
     return rec
 
 
@@ -406,21 +451,21 @@ def main_lti(a, rank, world, local, dist, dev):
     from solvempc_amd import dist as mdist
     from solvempc_amd import workload
 
-    N, B = a.horizon, a.batch
+    N = a.horizon
+    start, B, pad, total = blocks(a, rank, world)  # this rank's QPs (weak: --batch each; strong: a block of the job)
     plant = workload.reference_plant()
     ops = sm.mpc.condense({"Ad": plant["Ad"][None], "Bd": plant["Bd"][None], "Cd": plant["Cd"][None],
                            "K": plant["K"][None], "Q": [plant["Q"]], "R": [plant["R"]], "RD": [plant["RD"]]},
                           N, device=local)
     ops = {k: v[0] for k, v in ops.items()}
-    start, count = mdist.weak_block(B, rank)  # weak scaling: every rank owns B QPs of the global stream
     stream_mode = a.workload == "stream"
     perplant = a.workload == "perplant"
-    X, U = workload.stream_states(a.seed, start, count) if stream_mode else workload.mpc_states(a.seed, start, count)
+    X, U = workload.stream_states(a.seed, start, B) if stream_mode else workload.mpc_states(a.seed, start, B)
     l = np.full(2 * N, -np.finfo(np.float64).max)
     u0 = ops["W0"].copy()  # W0 + Sbar 0 + Ku 0 (:43)
 
     if perplant:  # config 3: every QP its own plant, condensed and set up on the device each step
-        Ad, Bd = workload.randomized_plants(plant, a.seed, start, count)
+        Ad, Bd = workload.randomized_plants(plant, a.seed, start, B)
         solver = sm.BatchSolver(N, 2 * N, B, B, a.dtype, local)
         tdev = lambda v: torch.as_tensor(np.ascontiguousarray(v, dtype=np.float64)).to(dev)  # noqa: E731
         plant_d = [tdev(Ad), tdev(Bd), tdev(np.tile(plant["Cd"], (B, 1))), tdev(np.tile(plant["K"], (B, 1))),
@@ -430,7 +475,8 @@ def main_lti(a, rank, world, local, dist, dev):
         solver.setup(ops["P"], np.zeros(N), ops["A"], l, u0)
         solver.mpc_set_operators(ops["Fx"], ops["Fu"], ops["Fr"], ops["Sbar"], ops["Ku"], ops["W0"])
     X_d = torch.from_numpy(X).to(dev)
-    U0_d = torch.from_numpy(U).to(dev)
+    U0_d = torch.zeros(pad, dtype=torch.float64, device=dev)  # (strong: padded to the longest block, gather)
+    U0_d[:B] = torch.from_numpy(U).to(dev)
     U_d = U0_d.clone()
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
@@ -473,7 +519,7 @@ def main_lti(a, rank, world, local, dist, dev):
 
     status, iters, rho_f = solver.info()
     kind, paired = solver.path()
-    qps_per_step = B * (a.ctrl_steps if stream_mode else 1)
+    qps_per_step = total * (a.ctrl_steps if stream_mode else 1)  # every rank's QPs of one bench step
     if stream_mode:  # iterations every QP ran over all control steps of the last bench step (device counters)
         it_total = solver.stream_iterations()
         flops = float(workload.flops_per_qp_total(N, 2 * N, 4, it_total, a.ctrl_steps, paired=paired).sum())
@@ -485,12 +531,12 @@ def main_lti(a, rank, world, local, dist, dev):
     solved = float(np.mean(status == sm.SOLVED))
     if rank != 0:
         return None
-    total_qps = qps_per_step * world * a.steps / wall
+    total_qps = qps_per_step * a.steps / wall
     config = ({"workload": f"cfg2: {B} identical LTI plants per GPU, N={N} (n={N}, m={2 * N}), one controllerStep each",
                "batch_per_gpu": B, "horizon": N, "parallelism": f"dp{world}"} if a.workload == "cfg2" else
-              {"workload": f"cfg3: {B} randomised plants per GPU (Ad, Bd +-2% ~ N(0,1), rho(Ad) < 1), N={N}: "
-                           f"on-device condensing + setup + one controllerStep each",
-               "batch_per_gpu": B, "horizon": N, "parallelism": f"dp{world}"} if perplant else
+              {"workload": f"cfg3: {total} randomised plants (Ad, Bd +-2% ~ N(0,1), rho(Ad) < 1), {B} on rank 0, "
+                           f"N={N}: on-device condensing + setup + one controllerStep each",
+               "batch_per_gpu": B, "global_batch": total, "horizon": N, "parallelism": f"dp{world}"} if perplant else
               {"workload": f"cfg5: {B} plants per GPU x {a.ctrl_steps} warm-started control steps, simulated plant "
                            f"(noise std {a.noise}, X0 ~ N(0, {workload.STREAM_X_SCALE}^2 diag(.1,.1,.05,.5)), U0 = 0), "
                            f"one launch for all steps (tile stream mode where the shape allows), N={N}",

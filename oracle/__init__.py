@@ -394,6 +394,8 @@ def stream_run(plant: dict, X, U, N: int, steps: int, seed: int, first_qp: int =
     Returns (X, U after the steps, per-plant iterations summed over the steps, unsolved steps)."""
     X, U = _c64(X).copy(), _c64(U).copy()
     k, nx = X.shape
+    if not (1 <= N <= 64 and 1 <= nx <= 8):
+        raise ValueError(f"stream_run: 1 <= N <= 64 and 1 <= nx <= 8 (got N={N}, nx={nx})")
     s = settings or default_settings()
     it = np.zeros(k, dtype=np.int32)
     un = np.zeros(k, dtype=np.int32)

@@ -95,6 +95,7 @@ int ora_stream_run(int batch, int nx, int N, int s_rows, const double *Ad, const
                    long long first_step, double noise_std, int *it_total, int *unsolved, int nthreads)
 {
     const int n = N, m = 2 * N;
+    if (N < 1 || N > 64 || nx < 1 || nx > 8) return -2; /* the per-thread q[64], u[128], xn[8] below */
     double *buf = (double *)malloc(sizeof(double) * (size_t)(5 * N * N + 4 * N * nx + 16 * N + 8 * m));
     double *P = buf, *A = P + N * N, *Fx = A + 2 * N * N, *Fu = Fx + N * nx, *Fr = Fu + N;
     double *Sbar = Fr + N * N, *Ku = Sbar + 2 * N * nx, *W0 = Ku + 2 * N, *Su = W0 + 2 * N;

@@ -286,6 +286,26 @@ int check_ctx(mpcq_ctx *c, Need need)
     return MPCQ_OK;
 }
 
+// The plants' setup data and operator blocks (generic setups; mimo-only contexts keep one unused block)
+int ensure_plant_buffers(mpcq_ctx *c)
+{
+    if (c->d_ops) return MPCQ_OK;
+    const size_t Pg = c->mimo_only ? 1 : c->dims.n_plants, n = c->dims.n, m = c->dims.m;
+    const mpcq::OpsLayout L = mpcq::OpsLayout::make(c->nc, c->mc);
+    void **ptrs[] = {(void **)&c->d_P, (void **)&c->d_q0, (void **)&c->d_A, (void **)&c->d_l0, (void **)&c->d_u0,
+                     (void **)&c->d_ops, (void **)&c->d_ops32, (void **)&c->d_ctype};
+    const size_t bytes[] = {8 * Pg * n * n, 8 * Pg * n, 8 * Pg * m * n, 8 * Pg * m, 8 * Pg * m, 8 * Pg * L.total,
+                            c->dims.dtype == MPCQ_F32 ? 4 * Pg * L.total : 0, 4 * Pg * c->mc};
+    for (int i = 0; i < 8; i++) {
+        if (!bytes[i] || *ptrs[i]) continue;
+        if (hipMalloc(ptrs[i], std::max<size_t>(bytes[i], 8)) != hipSuccess) {
+            *ptrs[i] = nullptr;
+            return fail(MPCQ_ERR_HIP, "hipMalloc failed (plant setup buffers)");
+        }
+    }
+    return MPCQ_OK;
+}
+
 // Generic entry points that only need the device and the generic buffers (no setup yet)
 int check_generic_dims(mpcq_ctx *c)
 {
@@ -393,15 +413,12 @@ int mpcq_create(const mpcq_dims *d, const mpcq_settings *s, mpcq_ctx **out)
         if (!ok) return;
         if (hipMalloc(p, std::max<size_t>(bytes, 8)) != hipSuccess) ok = false;
     };
-    const size_t Pg = c->mimo_only ? 1 : P;  // mimo-only: the generic setup arrays are unused
-    A((void **)&c->d_P, 8 * Pg * n * n);
-    A((void **)&c->d_q0, 8 * Pg * n);
-    A((void **)&c->d_A, 8 * Pg * m * n);
-    A((void **)&c->d_l0, 8 * Pg * m);
-    A((void **)&c->d_u0, 8 * Pg * m);
-    A((void **)&c->d_ops, 8 * Pg * L.total);
-    if (d->dtype == MPCQ_F32) A((void **)&c->d_ops32, 4 * Pg * L.total);
-    A((void **)&c->d_ctype, 4 * Pg * mc);
+    // a shared plant's setup arrays now; per-plant ones at the first setup (ensure_plant_buffers): a
+    // one-pass context (mpcq_mpc_plants_step_device, ~1M plants on one GPU) never allocates them
+    if (P == 1 && !(ok = ensure_plant_buffers(c) == MPCQ_OK)) {
+        mpcq_destroy(c);
+        return fail(MPCQ_ERR_HIP, "hipMalloc failed");
+    }
     A((void **)&c->d_setup_status, 4 * P);
     A((void **)&c->d_flags, 4);
     A((void **)&c->d_q, 8 * B * n);
@@ -584,6 +601,7 @@ int mpcq_setup(mpcq_ctx *c, const double *P, const double *q0, const double *A, 
     if (!P || !q0 || (m && (!A || !l0 || !u0))) return fail(MPCQ_ERR_ARG, "null setup array");
     for (size_t i = 0; i < Pn * m; i++)
         if (l0[i] > u0[i]) return fail(MPCQ_ERR_BOUNDS, "lower bound above upper bound (osqp validate_data)");
+    if ((rc = ensure_plant_buffers(c))) return rc;
     c->mode = mpcq_ctx::Mode::None;
     // rows n + j of A are the negated rows j (the reference's Gbar = [K0 L; -K0 L],
     // ModelPredictiveControlAPI.cpp:332-347), checked bit for bit: the tile kernel's paired loop
@@ -1452,6 +1470,7 @@ int mpcq_mpc_setup_plants_device(mpcq_ctx *c, int nx, int s_rows, const double *
     if (nx <= 0 || nx > 8 || s_rows < 0) return fail(MPCQ_ERR_ARG, "setup_plants: 1 <= nx <= 8, s_rows >= 0");
     if (m != 2 * n) return fail(MPCQ_ERR_ARG, "MPC front end needs m == 2n (ModelPredictiveControlAPI.cpp:47-48)");
     if (!Ad || !Bd || !Cd || !K || !Q || !R || !RD) return fail(MPCQ_ERR_ARG, "setup_plants: null plant array");
+    if ((rc = ensure_plant_buffers(c))) return rc;
     if ((rc = materialize_qu(c))) return rc;  // (with the operators the pending step used)
     if (!alloc_mpc_ops(c, nx)) return fail(MPCQ_ERR_HIP, "hipMalloc failed");
     c->nx = nx;

@@ -88,3 +88,26 @@ def test_bench_launches_its_own_ranks():
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["steps"] == 3 and rec["dry_run"] is True
     assert rec["collective"] == {"backend": "gloo", "world_size": 2, "gathered": 2000, "matches_stream": True}
+    assert rec["scaling"] == "weak"
+
+
+def test_bench_strong_scaling_splits_one_global_batch():
+    """BASELINE config 3 as written: `--workload perplant --scaling strong` splits ONE global batch
+    (here 1,001 plants, not a multiple of the world size) into contiguous blocks (dist.strong_block);
+    the gather pads every block to the longest and rank 0 recovers exactly the global stream."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2", "--backend", "gloo", "--dry-run",
+                        "--workload", "perplant", "--scaling", "strong", "--global-batch", "1001",
+                        "--steps", "2", "--warmup", "1"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert rec["scaling"] == "strong" and rec["config"]["global_batch"] == 1001
+    assert rec["config"]["batch_per_gpu"] == 501  # rank 0's block
+    assert rec["collective"]["gathered"] == 1001 and rec["collective"]["matches_stream"] is True
+    assert 1 << 20 == __import__("bench").parse(["--workload", "perplant", "--scaling", "strong"]).global_batch

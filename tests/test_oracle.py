@@ -228,3 +228,15 @@ def test_stream_run_matches_python_replay(plant):
     assert np.array_equal(it, its) and np.all(un == 0)
     np.testing.assert_allclose(Uc, Uk, rtol=0, atol=1e-12)
     np.testing.assert_allclose(Xc, Xk, rtol=0, atol=1e-12)
+
+
+def test_stream_run_rejects_shapes_beyond_its_buffers(plant):
+    """ora_stream_run keeps q, u, x_next per thread in fixed buffers (N <= 64, nx <= 8): larger shapes are
+    rejected, not written past the end."""
+    import pytest
+
+    X, U = np.zeros((2, 4)), np.zeros(2)
+    with pytest.raises(ValueError):
+        oracle.stream_run(plant, X, U, 65, 1, 4)
+    with pytest.raises(ValueError):
+        oracle.stream_run(plant, np.zeros((2, 9)), U, 20, 1, 4)
