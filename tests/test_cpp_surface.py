@@ -12,6 +12,7 @@
 * the ``solvempc`` CLI (solver.cpp surface) fails loudly without a device or a readable config.
 """
 import json
+import os
 import subprocess
 from pathlib import Path
 
@@ -35,6 +36,8 @@ def _has_gpu():
 
 @pytest.fixture(scope="module")
 def from_json_check():
+    if os.environ.get("FROM_JSON_CHECK"):  # the ASan / UBSan build (make sanitize)
+        return Path(os.environ["FROM_JSON_CHECK"])
     subprocess.run(["make", "-C", str(CPP), "-s", "build/from_json_check"], check=True)
     return CPP / "build" / "from_json_check"
 
