@@ -723,6 +723,47 @@ def test_stream_workload_stays_solved_and_bounded(plant):
     assert np.abs(Xd.cpu().numpy()).max() < 10 and np.abs(Ud.cpu().numpy()).max() < 10
 
 
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_stream_bench_path_matches_oracle(plant, dtype, monkeypatch):
+    """The config-5 bench path itself (one tile-stream launch, 4 plants per wave as the bench's 4,096-plant
+    batch runs it) at 512 plants x 1,000 warm-started control steps against oracle.stream_run (one
+    warm-started OSQP-0.6 restatement per plant on the device's noise stream): every step of every plant
+    SOLVED on both sides; fp64: every plant's iteration total equal and the final U within 1e-8; fp32
+    (the bench's dtype, whose closed loops drift from the fp64 ones by rounding over 1,000 steps): the
+    iteration totals equal on >= 99 % of plants (the rest: an fp32 schedule tie somewhere in the 1,000
+    steps, within 1 % of the total) and the final U within 1e-3."""
+    import torch
+    monkeypatch.setenv("MPCQ_STREAM_CPW", "4")
+    N, B, steps, seed, noise = 20, 512, 1000, 4, 1e-2
+    ops = oracle.condense(plant, N)
+    l = np.full(2 * N, LMIN)
+    X, U = workload.stream_states(seed, 0, B)
+    s = sm.BatchSolver(N, 2 * N, B, dtype=dtype)
+    s.setup(ops["P"], np.zeros(N), ops["A"], l, oracle.upper_bound(ops, np.zeros(4), 0.0))
+    s.mpc_set_operators(ops["Fx"], ops["Fu"], ops["Fr"], ops["Sbar"], ops["Ku"], ops["W0"])
+    s.mpc_set_plant(plant["Ad"], plant["Bd"])
+    Xd, Ud = torch.from_numpy(X.copy()).cuda(), torch.from_numpy(U.copy()).cuda()
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        s.mpc_run_device(Xd.data_ptr(), Ud.data_ptr(), plant["xref"], steps, seed, 0, 0, noise, st.cuda_stream)
+    st.synchronize()
+    assert s.stream_path() == "tile"
+    it_dev, uns_dev = s.stream_iterations(), s.stream_unsolved()
+    Xc, Uc, itc, unc = oracle.stream_run(plant, X, U, N, steps, seed, 0, 0, noise, xref=plant["xref"])
+    assert uns_dev == 0 and int(unc.sum()) == 0
+    same = it_dev == itc
+    dU = np.abs(Ud.cpu().numpy() - Uc)
+    if dtype == "f64":
+        assert same.all(), np.flatnonzero(~same)[:8]
+        assert dU.max() < 1e-8 and np.abs(Xd.cpu().numpy() - Xc).max() < 1e-8
+    else:
+        assert same.mean() >= 0.99, same.mean()
+        assert (np.abs(it_dev - itc) / itc).max() < 0.01
+        assert dU.max() < 1e-3, dU.max()
+    print(f"stream {dtype}: {B} plants x {steps} steps, iteration totals equal on {same.mean():.4f}, "
+          f"max |dU| {dU.max():.2e}")
+
+
 @pytest.mark.parametrize("n,m", [(5, 7), (13, 30), (20, 40), (32, 64)])
 def test_per_plant_setups_agree(n, m):
     """Per-plant setup three ways on random convex QPs of odd and even order (equality rows, finite
