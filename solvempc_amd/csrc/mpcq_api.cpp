@@ -49,6 +49,7 @@ constexpr int kMaxPhases = 16;
 //   MPCQ_STREAM_CPW=k           plants per wave of the tile stream mode
 //   MPCQ_TAIL=wave|tile         the tile chain's last launch on the one-QP-per-wave / tile kernel
 //   MPCQ_MIX_R=r                MPCQ_F64_MIXED: fp64 iterations per check interval (default MPCQ_MIX_R)
+//   MPCQ_TILE_OCC=2|3           waves per SIMD of the f32 paired tile kernel (default 3)
 // Debug builds (-DMPCQ_DEBUG_HOOKS) add the stamp / profiling dumps (MPCQ_TILE_STAMPS,
 // MPCQ_SETUP_PROF, MPCQ_MIMO_SETUP_STAMPS, MPCQ_MIMO_STAMPS) and MPCQ_DEBUG_SYNC.
 const char *test_hook(const char *name)
@@ -220,6 +221,10 @@ mpcq::AdmmArgs<T> make_args(mpcq_ctx *c)
     a.iter = c->d_iter;
     a.it_acc = c->stream_acc ? c->d_it_acc : nullptr;
     a.uns_acc = c->stream_acc ? c->d_uns_acc : nullptr;
+    {
+        const char *o = test_hook("MPCQ_TILE_OCC");  // f32 paired tile kernel: 2 or 3 waves/SIMD (A/B)
+        a.tile_occ = *o ? std::atoi(o) : 0;
+    }
     if (c->dims.dtype == MPCQ_F64_MIXED) {  // (test hook MPCQ_MIX_R: another fp64 share for A/B)
         const char *r = test_hook("MPCQ_MIX_R");
         a.mix_r = *r ? std::max(1, std::atoi(r)) : MPCQ_MIX_R;

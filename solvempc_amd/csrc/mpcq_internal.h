@@ -202,6 +202,8 @@ struct AdmmArgs {
     // mixed precision (MPCQ_F64_MIXED contexts, the tile kernel's paired loop): the last mix_r iterations
     // before every info iteration run in fp64, the earlier plain ones in fp32 (0: all fp64)
     int mix_r;
+    // waves per SIMD of the f32 paired tile kernel (0: the default, 3; 2: the OCC-2 variant)
+    int tile_occ;
 };
 
 // MFMA operand images of one shared plant for the tile kernel (mpcq_tile.h).  A vector of length

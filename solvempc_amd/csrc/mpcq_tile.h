@@ -1741,13 +1741,15 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
 }
 
 // Launch one tile-kernel variant: one workgroup per 64 G QPs of the phase's grid.
+// lds_pad: dynamic LDS bytes on top of the kernel's static allocation (0, or enough that fewer
+// workgroups fit a CU: the occupancy A/B below)
 template <typename T, int KN, int KM, bool AI, bool LF, int G, int OCC, bool PAIRED = false, int WPB = 4, bool MIX = false>
-int tile_launch_variant(const AdmmArgs<T> &a, hipStream_t s)
+int tile_launch_variant(const AdmmArgs<T> &a, hipStream_t s, unsigned lds_pad = 0)
 {
     constexpr int QPW = 16 * G * WPB;
     const int blocks = (a.batch + QPW - 1) / QPW;
-    hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, AI, LF, G, OCC, PAIRED, WPB, false, MIX>), dim3(blocks), dim3(64 * WPB), 0,
-                       s, a);
+    hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, AI, LF, G, OCC, PAIRED, WPB, false, MIX>), dim3(blocks), dim3(64 * WPB),
+                       lds_pad, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -1778,6 +1780,11 @@ int tile_launch(const AdmmArgs<T> &a, hipStream_t s)
         if (a.paired && a.all_ineq && a.lower_free) {  // the condensed-MPC shape: paired, VGPR-resident loop
             if constexpr (std::is_same<T, double>::value) {
                 if (a.mix_r > 0) return tile_launch_variant<T, KN, KM, true, true, 1, OCC, true, 4, true>(a, s);
+            } else {
+                // f32 at 2 waves/SIMD (AdmmArgs::tile_occ): a batch of 2 k rounds of 2,048 wave slots runs
+                // without the lone-wave last round 3 waves/SIMD leave (4,096 waves on 3,072 slots); the
+                // registers allow 3, so dynamic LDS holds a CU to 2 workgroups (> 160 KiB / 3 each)
+                if (a.tile_occ == 2) return tile_launch_variant<T, KN, KM, true, true, 1, OCC, true>(a, s, 16 * 1024);
             }
             return tile_launch_variant<T, KN, KM, true, true, 1, OCC, true>(a, s);
         }
