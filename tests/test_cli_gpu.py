@@ -93,9 +93,12 @@ def test_cli_replay_matches_oracle_controller(tmp_path, plant):
     assert log.count("status:               solved\n") == steps
     its = [int(v) for v in re.findall(r"number of iterations: (\d+)", log)]
     assert its == _oracle_wire.iters
-    for row in re.findall(r"iter   objective    pri res    dua res    rho        time\n(.*)\n", log):
+    rows = re.findall(r"iter   objective    pri res    dua res    rho        time\n(.*)\n", log)
+    assert len(rows) == steps
+    for row, want in zip(rows, _oracle_wire.iters):
         it, obj, pri, dua, rho, t = row.split()
-        assert float(pri) <= 1e-3 * 10 and float(dua) <= 1e-3 * 10 and t.endswith("s")
+        assert int(it) == want and np.isfinite(float(obj)) and float(pri) >= 0 and float(dua) >= 0
+        assert float(rho) > 0 and t.endswith("s")
 
 
 def test_reference_shaped_eigen_caller_on_device(tmp_path, plant):
