@@ -16,7 +16,7 @@ import numpy as np
 
 from . import _capi
 from ._capi import (  # noqa: F401
-    MPCQ_F32, MPCQ_F64, MPCQ_F64_MIXED, SOLVED, SOLVED_INACCURATE, MAX_ITER_REACHED, PRIMAL_INFEASIBLE,
+    MPCQ_F32, MPCQ_F64, MPCQ_F64_MIXED, MPCQ_MIX_R, SOLVED, SOLVED_INACCURATE, MAX_ITER_REACHED, PRIMAL_INFEASIBLE,
     PRIMAL_INFEASIBLE_INACCURATE, DUAL_INFEASIBLE, DUAL_INFEASIBLE_INACCURATE, NON_CVX, UNSOLVED,
     INVALID_BOUNDS, TYPE_CHANGED, MpcqError, Settings, lib, library_path,
 )
