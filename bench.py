@@ -44,8 +44,11 @@ def parse(argv=None):
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--batch", type=int, default=65536, help="QPs per GPU")
     p.add_argument("--horizon", type=int, default=20)
-    p.add_argument("--dtype", choices=("f64", "f32", "mixed"), default="f32",
-                   help="ADMM iterate type (BASELINE cfg 2: fp32; mixed: MPCQ_F64_MIXED, the north-star tolerance)")
+    p.add_argument("--dtype", choices=("f64", "f32", "mixed"), default=None,
+                   help="ADMM arithmetic (default: mixed for cfg2, the fastest path inside north_star's 1e-5 on "
+                        "the applied move; f32 for the other LTI workloads; quadrotor is f64)")
+    p.add_argument("--variants", type=int, default=1,
+                   help="cfg2: also time the f32 and f64 paths on the same batch (the line's `variants` block)")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=0, help="threads of the multi-threaded CPU leg (0: all usable)")
@@ -67,6 +70,8 @@ def parse(argv=None):
     p.add_argument("--dry-run", action="store_true",
                    help="no device: launcher, rendezvous and the gather only (CPU tests of the N > 1 plumbing)")
     a = p.parse_args(argv)
+    if a.dtype is None:
+        a.dtype = "mixed" if a.workload == "cfg2" else "f32"
     if a.workload == "stream" and a.batch == 65536:
         a.batch = 4096
     if a.workload == "perplant" and a.batch == 65536:
@@ -516,8 +521,38 @@ def main_lti(a, rank, world, local, dist, dev):
 
     wall, got = _timed_loop(a, step, dist, world, dev)
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    U_out = U_d[:B].cpu().numpy().copy()  # this step's applied U (the parity block's device side)
 
     status, iters, rho_f = solver.info()
+    # cfg2 at N = 1: the other precisions on the same batch with the same protocol (the `variants` block)
+    variants = {}
+    if a.workload == "cfg2" and a.variants and world == 1 and a.scaling == "weak":
+        for vdt in [d for d in ("f32", "mixed", "f64") if d != a.dtype]:
+            vs = sm.BatchSolver(N, 2 * N, B, 1, vdt, local)
+            vs.setup(ops["P"], np.zeros(N), ops["A"], l, u0)
+            vs.mpc_set_operators(ops["Fx"], ops["Fu"], ops["Fr"], ops["Sbar"], ops["Ku"], ops["W0"])
+            vev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+
+            def vstep(i=None, vs=vs, vev=vev):
+                U_d.copy_(U0_d)
+                vs.reset_state()
+                if i is not None:
+                    vev[i][0].record(stream)
+                vs.mpc_step_device(X_d.data_ptr(), U_d.data_ptr(), plant["xref"], sptr)
+                if i is not None:
+                    vev[i][1].record(stream)
+                return [U_d]
+
+            vwall, _ = _timed_loop(a, vstep, dist, world, dev)
+            vst, vit, _ = vs.info()
+            vkind, vpaired = vs.path()
+            vflops = float(workload.flops_per_qp(N, 2 * N, 4, vit, paired=vpaired).sum())
+            vms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in vev]))
+            variants[vdt] = {"dtype": DTYPE_NAME[vdt], "value": B * a.steps / vwall, "ms_per_step": vwall / a.steps * 1e3,
+                             "kernel_ms": vms, "achieved_tflops": vflops / (vms * 1e-3) / 1e12,
+                             "iters_mean": float(vit.mean()), "solved_frac": float(np.mean(vst == sm.SOLVED)),
+                             "_U": U_d[:B].cpu().numpy().copy(), "_it": vit}
+            vs.close()
     kind, paired = solver.path()
     qps_per_step = total * (a.ctrl_steps if stream_mode else 1)  # every rank's QPs of one bench step
     if stream_mode:  # iterations every QP ran over all control steps of the last bench step (device counters)
@@ -617,7 +652,7 @@ def main_lti(a, rank, world, local, dist, dev):
         rec["parity"] = {"plants": int(ns), "steps": a.ctrl_steps,
                          "it_total_match": float(np.mean(it_total[:ns] == itc)),
                          "it_total_rel_diff": float(np.abs(it_total[:ns] - itc).sum() / max(1, itc.sum())),
-                         "max_abs_dU_final": float(np.abs(U_d[:ns].cpu().numpy() - Uc).max()),
+                         "max_abs_dU_final": float(np.abs(U_out[:ns] - Uc).max()),
                          "unsolved_steps_cpu": int(unc.sum())}
     if a.cpu_seconds > 0 and not stream_mode and world == 1:  # (rank 0 at N = 1 only)
         import oracle
@@ -634,10 +669,17 @@ def main_lti(a, rank, world, local, dist, dev):
             run = lambda n, t: oracle.batch_solve(ops["P"], ops["A"], q0, l, u0, q[:n], u[:n], nthreads=t)  # noqa: E731
             rec["cpu_baseline"], ns, (x_ref, st_ref, it_ref, _) = cpu_baseline(
                 "port", run, 256, B, a.cpu_seconds, a.cpu_threads, "oracle/osqp_dense.c (OSQP-0.6 restatement)")
-        du = U_d[:ns].cpu().numpy() - U[:ns]
+        du = U_out[:ns] - U[:ns]
         rec["parity"] = _parity(du, iters[:ns], x_ref, it_ref, st_ref)
         if perplant:
             rec["parity"].pop("max_rel_du0")  # (the per-plant oracle returns U only)
+        for v in variants.values():
+            v["parity"] = _parity(v["_U"][:ns] - U[:ns], v["_it"][:ns], x_ref, it_ref, st_ref)
+    if variants:
+        for v in variants.values():
+            v.pop("_U")
+            v.pop("_it")
+        rec["variants"] = variants
     return rec
 
 
