@@ -1262,6 +1262,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 // the operators rounded from the fp64 images; then the last mix_r - 1 plain iterations and
                 // the info iteration in fp64 (below)
                 const int n32 = nxt - a.mix_r;
+#ifdef MPCQ_MIX_STAMPS  // debug build: cycles in the fp32 stretches -> phase stamp 5
+                const long long t_mix = a.stamps ? (long long)__builtin_amdgcn_s_memtime() : 0;
+#endif
                 if (it < n32) {
                     float xs32[G][NS], z32[G][MS], y32[G][MS], uh32[G][MS], gv32[G][NS], rho32[G], adk32[G][KNR];
 #pragma unroll
@@ -1315,6 +1318,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                         }
                     }
                 }
+#ifdef MPCQ_MIX_STAMPS
+                if (a.stamps) info_cycles += (long long)__builtin_amdgcn_s_memtime() - t_mix;
+#endif
             }
             if (REMV && it + 1 < nxt) {
                 if constexpr (REMV) {

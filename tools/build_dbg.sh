@@ -6,11 +6,11 @@
 #        then MPCQ_LIBRARY=tools/dbglib/libmpcq.so MPCQ_TILE_STAMPS=out.bin python ...
 set -e
 cd "$(dirname "$0")/../solvempc_amd/csrc"
-mkdir -p ../../tools/dbglib
+D=../../${DBGDIR:-tools/dbglib}; mkdir -p $D
 SRC=${SRC:-mpcq_tile_f32.hip}
 DEFS="-DMPCQ_DEBUG_HOOKS $(for d in "$@"; do printf -- "-D%s " "$d"; done)"
 FL="-O3 -ffp-contract=off -fno-slp-vectorize -std=c++17 -fPIC --offload-arch=gfx950"
-/opt/rocm/bin/hipcc $FL $DEFS -c $SRC -o ../../tools/dbglib/dbg_src.o
-/opt/rocm/bin/hipcc $FL $DEFS -c mpcq_api.cpp -o ../../tools/dbglib/dbg_api.o
+/opt/rocm/bin/hipcc $FL $DEFS -c $SRC -o $D/dbg_src.o
+/opt/rocm/bin/hipcc $FL $DEFS -c mpcq_api.cpp -o $D/dbg_api.o
 objs=$(ls build/*.o | grep -v -e "$SRC" -e mpcq_api.cpp)
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ../../tools/dbglib/libmpcq.so $objs ../../tools/dbglib/dbg_src.o ../../tools/dbglib/dbg_api.o
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $D/libmpcq.so $objs $D/dbg_src.o $D/dbg_api.o
