@@ -33,9 +33,6 @@
 #ifndef MPCQ_PK
 #define MPCQ_PK 1  // build switch for A/B: 0 runs the f32 plain iterations on scalar VALU ops
 #endif
-#ifndef MPCQ_REMV
-#define MPCQ_REMV 1  // build switch for A/B: 0 runs the f64 remainder rows (16 .. 19) on the matrix cores
-#endif
 
 namespace mpcq {
 
@@ -228,24 +225,6 @@ __device__ __forceinline__ float rem_reduce(const Mf<float>::acc &p)
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);                // row g
 }
 
-// rem_reduce for f64 partials (each 32-bit half moved by its own lane swap): lane (g, c) holds
-// p_i = sum over k = g (mod 4) of row i of a 4-row remainder tile; returns row g on lane group g.
-__device__ __forceinline__ double rem_reduce64(double p0, double p1, double p2, double p3)
-{
-    auto lo = [](double v) { return (unsigned)(unsigned long long)__double_as_longlong(v); };
-    auto hi = [](double v) { return (unsigned)((unsigned long long)__double_as_longlong(v) >> 32); };
-    auto mk = [](unsigned l, unsigned h) { return __longlong_as_double((long long)(((unsigned long long)h << 32) | l)); };
-    auto a02 = __builtin_amdgcn_permlane32_swap(lo(p0), lo(p2), false, false);
-    auto b02 = __builtin_amdgcn_permlane32_swap(hi(p0), hi(p2), false, false);
-    auto a13 = __builtin_amdgcn_permlane32_swap(lo(p1), lo(p3), false, false);
-    auto b13 = __builtin_amdgcn_permlane32_swap(hi(p1), hi(p3), false, false);
-    const double q0 = mk(a02[0], b02[0]) + mk(a02[1], b02[1]);  // rows 0 | 2 (lanes 0-31 | 32-63)
-    const double q1 = mk(a13[0], b13[0]) + mk(a13[1], b13[1]);  // rows 1 | 3
-    auto a = __builtin_amdgcn_permlane16_swap(lo(q0), lo(q1), false, false);
-    auto b = __builtin_amdgcn_permlane16_swap(hi(q0), hi(q1), false, false);
-    return mk(a[0], b[0]) + mk(a[1], b[1]);  // row g
-}
-
 // The same product for G independent 16-QP groups of one wave: every A operand read from LDS feeds
 // G MFMAs, and the G accumulator chains interleave (more independent work per wave).
 // REM (f32, the last tile holds 4 real rows): that tile on v_mfma_f32_4x4x1_16b, its A fragment read
@@ -430,10 +409,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     // q^ of each wave's QPs (lane layout): the dual residual of every check iteration reads it here
     // instead of re-reading q (fp64, HBM) under the latency of a loaded memory system
     __shared__ T s_qh[WPB][G * KN][64];
-    // f64 paired loop (REMV): the remainder rows 16 .. 19 of S, B~', B~ as [product][g][row i][k-step s]
-    // = M[16 + i][4 s + g], for the VALU half of the products (built from the images after the barrier)
-    constexpr bool REMV = PAIRED && std::is_same<T, double>::value && L.NT == 2 && KN == 5 && MPCQ_REMV;
-    __shared__ __attribute__((aligned(16))) double s_rem[REMV ? 3 : 1][4][4][REMV ? 6 : 1];
     T *const s_lam = rowv, *const s_D = rowv + NCP, *const s_Dinv = rowv + 2 * NCP;
     T *const s_E = rowv + 3 * NCP, *const s_Einv = rowv + 3 * NCP + MCP;
     // resumed phase: this workgroup serves list segment `seg` (ListSeg), as its workgroup `blk`
@@ -514,15 +489,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                     if (t < n) s2 += fr[t] * a.xref;
                 fe[FE_FR + v] = s2;
             }
-        }
-    }
-    if constexpr (REMV) {  // (images in LDS already: read back after their stores' barrier below)
-        __syncthreads();
-        for (int e = threadIdx.x; e < 3 * 4 * 4 * KN; e += NTH) {
-            const int pr = e / (16 * KN), g4 = (e / (4 * KN)) % 4, i4 = (e / KN) % 4, sk = e % KN;
-            const size_t base = pr == 0 ? L.S : pr == 1 ? L.Bt : L.B;
-            const int ksp = pr == 1 ? KMP : KNP;
-            s_rem[pr][g4][i4][sk] = img[base + TileLayout::at(ksp, VEC, 1, sk, 16 * g4 + i4)];
         }
     }
     __syncthreads();  // the only barrier: waves are independent from here on
@@ -1043,76 +1009,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 }
         }
     };
-    // REMV (f64 paired loop, n = 20): y = init + M x with rows 0 .. 15 on the matrix cores (the tile-0
-    // fragments r0 in VGPRs) and the 4 remainder rows on the VALU: lane (g, c) sums its own k = 4 s + g
-    // terms of each remainder row (operators from s_rem, broadcast within a lane group), rem_reduce64
-    // folds the four lane groups.  An f64 16x16x4 MFMA takes 64 cycles whichever rows are real; the
-    // remainder tile's 5 of them per product become 20 FMAs and 6 lane swaps.
-    auto mv_remv = [&](const T (&r0)[1][KNR], const auto &x, const T (*init)[NS], const int pid, T (&y)[G][NS]) {
-        if constexpr (REMV) {
-            using A = typename Mf<T>::acc;
-            A acc[G];
-#pragma unroll
-            for (int gi = 0; gi < G; gi++)
-#pragma unroll
-                for (int r = 0; r < 4; r++) acc[gi][r] = init ? init[gi][r] : T(0);
-#pragma unroll
-            for (int sk = 0; sk < KN; sk++)
-#pragma unroll
-                for (int gi = 0; gi < G; gi++) acc[gi] = Mf<T>::mma(r0[0][sk], x[gi][sk], acc[gi]);
-            const double *R = fresh_ptr(&s_rem[pid][opaque((int)(threadIdx.x >> 4) & 3)][0][0]);
-#pragma unroll
-            for (int gi = 0; gi < G; gi++) {
-                double pr[4];
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    double t = 0.0;
-#pragma unroll
-                    for (int sk = 0; sk < KN; sk++) t = tt_fma(R[i * 6 + sk], (double)x[gi][sk], t);
-                    pr[i] = t;
-                }
-                const double rr = rem_reduce64(pr[0], pr[1], pr[2], pr[3]);
-#pragma unroll
-                for (int r = 0; r < 4; r++) y[gi][r] = acc[gi][r];
-                y[gi][4] = init ? init[gi][4] + rr : rr;
-#pragma unroll
-                for (int r = 5; r < NS; r++) y[gi][r] = T(0);
-            }
-        }
-    };
-    auto piter_remv = [&](const T (&rS0)[1][KNR], const T (&rBt0)[1][KNR], const T (&rB0)[1][KNR], T (&sx)[G][NS],
-                          const T (&adk)[G][KNR]) {
-        if constexpr (REMV) {
-            T wt[G][KNR];
-#pragma unroll
-            for (int gi = 0; gi < G; gi++)
-#pragma unroll
-                for (int s = 0; s < KN; s++)
-                    wt[gi][s] = rho[gi] * ((z[gi][s] - y[gi][s]) - (z[gi][s + KN] - y[gi][s + KN]));
-            T xi[G][NS];
-            mv_remv(rBt0, wt, sx, 1, xi);  // xi = (-g + S x') + B~' w~
-#pragma unroll
-            for (int gi = 0; gi < G; gi++)
-#pragma unroll
-                for (int s = 0; s < KN; s++) {
-                    xi[gi][s] = adk[gi][s] * xi[gi][s];
-                    xs[gi][s] = tt_fma(oma, xs[gi][s], xi[gi][s]);
-                }
-            T zt[G][NS];
-            mv_remv(rB0, xi, nullptr, 2, zt);  // alpha z~_top = B~ eta'
-            mv_remv(rS0, xs, gv, 0, sx);       // next: -g + S x'
-#pragma unroll
-            for (int gi = 0; gi < G; gi++)
-#pragma unroll
-                for (int s = 0; s < KM; s++) {
-                    const T v = s < KN ? tt_fma(oma, z[gi][s], zt[gi][s]) : tt_fma(oma, z[gi][s], -zt[gi][s - KN]);
-                    const T t = v + y[gi][s];
-                    const T zn = vmin(t, uh[gi][s]);
-                    y[gi][s] = t - zn;
-                    z[gi][s] = zn;
-                }
-        }
-    };
     // piter_fast's f32 arithmetic on packed pairs (v_pk_fma/add/mul_f32: two elements per VALU issue,
     // the f32 vector and matrix work share the SIMD's issue time): element pairs (2k, 2k + 1) of each
     // half-vector (top rows s < KN, bottom rows KN + s) with an odd last element on its own.  The state
@@ -1322,37 +1218,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 if (a.stamps) info_cycles += (long long)__builtin_amdgcn_s_memtime() - t_mix;
 #endif
             }
-            if (REMV && it + 1 < nxt) {
-                if constexpr (REMV) {
-                    T rS0[1][KNR], rBt0[1][KNR], rB0[1][KNR];  // tile-0 fragments only
-                    {
-                        const T *im = fresh_ptr((const T *)img);
-#pragma unroll
-                        for (int k = 0; k < KNR; k++) {
-                            rS0[0][k] = im[L.S + TileLayout::at(KNP, VEC, 0, k, lane)];
-                            rBt0[0][k] = im[L.Bt + TileLayout::at(KMP, VEC, 0, k, lane)];
-                            rB0[0][k] = im[L.B + TileLayout::at(KNP, VEC, 0, k, lane)];
-                        }
-                    }
-                    T sx[G][NS], adk[G][KNR];
-                    mv_remv(rS0, xs, gv, 0, sx);
-#pragma unroll
-                    for (int gi = 0; gi < G; gi++) {
-#pragma unroll
-                        for (int s = 0; s < KN; s++) adk[gi][s] = alpha * dk[gi][s];
-#pragma unroll
-                        for (int s = 0; s < KM; s++) y[gi][s] = y[gi][s] * rinv[gi];  // y -> yt = y / rho
-                    }
-                    do {
-                        it++;
-                        piter_remv(rS0, rBt0, rB0, sx, adk);
-                    } while (it + 1 < nxt);
-#pragma unroll
-                    for (int gi = 0; gi < G; gi++)
-#pragma unroll
-                        for (int s = 0; s < KM; s++) y[gi][s] = y[gi][s] * rho[gi];  // yt -> y
-                }
-            } else if (it + 1 < nxt) {
+            if (it + 1 < nxt) {
                 T rS[NTR][KNR], rBt[NTR][KNR], rB[NTR][KNR];
                 load_regs(rS, rBt, rB);
                 T sx[G][NS], adk[G][KNR];
