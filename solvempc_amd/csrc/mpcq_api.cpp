@@ -50,6 +50,7 @@ constexpr int kMaxPhases = 16;
 //   MPCQ_TAIL=wave|tile         the tile chain's last launch on the one-QP-per-wave / tile kernel
 //   MPCQ_MIX_R=r                MPCQ_F64_MIXED: fp64 iterations per check interval (default MPCQ_MIX_R)
 //   MPCQ_TILE_OCC=2|3           waves per SIMD of the f32 paired tile kernel (default 3)
+//   MPCQ_PLANT_WPE=2|3          waves per SIMD of the one-pass per-plant kernel (default 2)
 // Debug builds (-DMPCQ_DEBUG_HOOKS) add the stamp / profiling dumps (MPCQ_TILE_STAMPS,
 // MPCQ_SETUP_PROF, MPCQ_MIMO_SETUP_STAMPS, MPCQ_MIMO_STAMPS) and MPCQ_DEBUG_SYNC.
 const char *test_hook(const char *name)
@@ -439,8 +440,7 @@ int mpcq_create(const mpcq_dims *d, const mpcq_settings *s, mpcq_ctx **out)
     A(&c->d_ys, es * B * mc);
     A(&c->d_rhos, es * B);
     if (tile) {
-        const mpcq::TileLayout TL = mpcq::TileLayout::make(KN, KM, (int)(16 / es));
-        A(&c->d_img, es * TL.total);
+        A(&c->d_img, es * mpcq::TileLayout::buffer(KN, KM, (int)(16 / es)));
         const size_t lcap = (size_t)mpcq::ListSeg::kShards * mpcq::ListSeg::cap(B);  // entries per phase list
         A((void **)&c->d_list, 4 * 2 * lcap);
         A((void **)&c->d_counts, 4 * kMaxPhases * mpcq::ListSeg::kCounters);
@@ -1532,6 +1532,10 @@ int mpcq_mpc_plants_step_device(mpcq_ctx *c, int nx, int s_rows, const double *A
     a.adaptive_interval = c->set.adaptive_rho_interval ? c->set.adaptive_rho_interval : (ct ? 4 * ct : 100);
     a.x = c->d_x; a.y = c->d_y; a.rho_out = c->d_rho; a.status = c->d_status; a.iter = c->d_iter;
     a.flags = c->d_flags;
+    {
+        const char *w = test_hook("MPCQ_PLANT_WPE");  // (A/B: the 3-waves/SIMD variant)
+        a.wpe = *w ? std::atoi(w) : 2;
+    }
     const int lr = mpcq_internal_plant_step_launch(&a, c->dims.dtype == MPCQ_F32, s);
     if (lr) return fail(lr == -1 ? MPCQ_ERR_ARG : MPCQ_ERR_HIP, "plants_step kernel launch failed");
     c->mode = mpcq_ctx::Mode::OneShot;  // results only: no operator blocks were written

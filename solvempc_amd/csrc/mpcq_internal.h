@@ -210,25 +210,40 @@ struct AdmmArgs {
 // 4*KS is held in "D-layout": lane l = 16 g + c (column c = QP, group g) keeps element 4 s + g of
 // its QP in register s.  Image (tile t, k-step s, lane l) = M[16 t + arow(l & 15)][4 s + (l >> 4)],
 // stored [t][s / VEC][lane][s % VEC] so one lane reads VEC consecutive k-steps with one 16-B load.
+// paired (the tile kernel's paired loop, m = 2n, rows n + j of A = -rows j): only the top halves are
+// kept, B~ = B's first n rows and B~' = its transpose, A~' = the first n columns of A^' (KBT = KNP
+// k-steps, NT tiles), plus for f64 (VEC 2) BS = [B~; S] stacked (B~ rows 0 .. 4 KN - 1, then S): the
+// plain iteration's z~ = B~ eta' and S eta' in one product (ceil(8 KN / 16) tiles instead of 2 NT).
+// The buffer holds the generic set (make(.., false)) followed by the paired one (make(.., true)).
 struct TileLayout {
-    int KN, KM, NT, MT, VEC, KNP, KMP;
-    size_t S, Bt, B, PW, AhT, W, Wt, total;
-    __host__ __device__ static constexpr TileLayout make(int KN, int KM, int VEC)
+    int KN, KM, NT, MT, VEC, KNP, KMP, KBT, NBS;
+    bool paired;
+    size_t S, Bt, B, PW, AhT, W, Wt, BS, total;
+    __host__ __device__ static constexpr TileLayout make(int KN, int KM, int VEC, bool paired = false)
     {
         TileLayout L{};
-        L.KN = KN; L.KM = KM; L.VEC = VEC;
+        L.KN = KN; L.KM = KM; L.VEC = VEC; L.paired = paired;
         L.NT = (KN + 3) / 4; L.MT = (KM + 3) / 4;
         L.KNP = (KN + VEC - 1) / VEC * VEC; L.KMP = (KM + VEC - 1) / VEC * VEC;
+        L.KBT = paired ? L.KNP : L.KMP;
+        L.NBS = (paired && VEC == 2) ? (8 * KN + 15) / 16 : 0;
+        const int BT = paired ? L.NT : L.MT;  // tiles of B
         size_t o = 0;
         L.S = o;   o += (size_t)L.NT * L.KNP * 64;   // sigma W'W       (n x n)
-        L.Bt = o;  o += (size_t)L.NT * L.KMP * 64;   // B' = (A^ W)'    (n x m)
-        L.B = o;   o += (size_t)L.MT * L.KNP * 64;   // B = A^ W        (m x n)
+        L.Bt = o;  o += (size_t)L.NT * L.KBT * 64;   // B' = (A^ W)'    (n x m; paired n x n)
+        L.B = o;   o += (size_t)BT * L.KNP * 64;     // B = A^ W        (m x n; paired n x n)
         L.PW = o;  o += (size_t)L.NT * L.KNP * 64;   // P^ W            (n x n)
-        L.AhT = o; o += (size_t)L.NT * L.KMP * 64;   // A^'             (n x m)
+        L.AhT = o; o += (size_t)L.NT * L.KBT * 64;   // A^'             (n x m; paired n x n)
         L.W = o;   o += (size_t)L.NT * L.KNP * 64;   // W               (n x n)
         L.Wt = o;  o += (size_t)L.NT * L.KNP * 64;   // W'              (n x n)
+        L.BS = o;  o += (size_t)L.NBS * L.KNP * 64;  // [B~; S]         (8 KN x n; paired f64 only)
         L.total = o;
         return L;
+    }
+    // elements of the device buffer: both sets
+    __host__ __device__ static constexpr size_t buffer(int KN, int KM, int VEC)
+    {
+        return make(KN, KM, VEC, false).total + make(KN, KM, VEC, true).total;
     }
     __host__ __device__ static constexpr size_t at(int KSP, int VEC, int t, int s, int lane)
     {
@@ -329,6 +344,7 @@ struct PlantStepArgs {
     double *x, *y, *rho_out;                       // [plant] n, 2n unscaled solution; final rho
     int *status, *iter;
     int *flags;                                    // OR: 1 a plant's KKT matrix is not positive definite
+    int wpe;                                       // waves per SIMD of the kernel variant (2; 3: A/B hook)
 };
 }  // namespace mpcq
 

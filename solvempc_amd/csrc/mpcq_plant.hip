@@ -163,11 +163,9 @@ __device__ __forceinline__ bool gj_rows(double (&row)[NC], double *piv, int n, i
     return ok;
 }
 
-template <typename T, int NC>
-#ifndef MPCQ_PLANT_WPE
-#define MPCQ_PLANT_WPE 2
-#endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? MPCQ_PLANT_WPE : 2, NC <= 20 ? 8 : 4))) void plant_step_kernel(PlantStepArgs a)
+// WPE: waves per SIMD the register allocation is held to (2, or 3 for A/B: MPCQ_PLANT_WPE)
+template <typename T, int NC, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? WPE : 2, NC <= 20 ? 8 : 4))) void plant_step_kernel(PlantStepArgs a)
 {
     static_assert(NC % 4 == 0, "broadcast rows are read 16 B at a time");
     constexpr int LD = NC + 1;
@@ -377,7 +375,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? M
     // An iteration: x~ = g + Srow x + Btc (w_top - w_bot) (one broadcast round: the (A^ M^-1) product
     // formed in fp64 keeps the fp32 iterate as accurate as the dense operators), z~ = A^ x~ (a prefix
     // scan).
-    T Srow[NC], Btc[NC];
+    // fp64 (MERGED): one GEMV per iteration, x~ = g + M^-1 (sigma x + A^'(w_top - w_bot)) with A^' w a suffix
+    // scan (A^ = E K0 L D): row r of M^-1 in Srow, no Btc (half the FMAs, one broadcast, 40 VGPRs fewer).
+    // fp32 keeps the two products, (A^ M^-1)' formed in fp64.
+    constexpr bool MERGED = std::is_same<T, double>::value;
+    T Srow[NC], Btc[MERGED ? 1 : NC];
     T gk = T(0);
     const double Dd = lr ? Dr : 0.0, A2 = 2.0 * K0 * K0;
     auto factor = [&](double rho) -> bool {
@@ -402,12 +404,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? M
             const double2 e2 = *(const double2 *)(S.Ev + j);
             g = fma(row[j], q2.x, g);
             g = fma(row[j + 1], q2.y, g);
-            Srow[j] = (T)(st.sigma * row[j]);
-            Srow[j + 1] = (T)(st.sigma * row[j + 1]);
-            pre += d2.x * row[j];
-            Btc[j] = (T)((e2.x * K0) * pre);
-            pre += d2.y * row[j + 1];
-            Btc[j + 1] = (T)((e2.y * K0) * pre);
+            if constexpr (MERGED) {
+                Srow[j] = (T)row[j];
+                Srow[j + 1] = (T)row[j + 1];
+            } else {
+                Srow[j] = (T)(st.sigma * row[j]);
+                Srow[j + 1] = (T)(st.sigma * row[j + 1]);
+                pre += d2.x * row[j];
+                Btc[j] = (T)((e2.x * K0) * pre);
+                pre += d2.y * row[j + 1];
+                Btc[j + 1] = (T)((e2.y * K0) * pre);
+            }
         }
         gk = lr ? (T)(-g) : T(0);
         return ok;
@@ -422,6 +429,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? M
     const T alpha = (T)st.alpha, oma = T(1) - (T)st.alpha;
     const T ET = (T)(lr ? Er : 0.0), DT = (T)Dd, K0T = (T)K0;
     const T EK = ET * K0T;  // (A^ x)_r = E_r K0 sum_{k<=r} D_k x_k
+    const T sigT = (T)st.sigma;
     const bool scaled_term = st.scaled_termination != 0;
     const int ct = st.check_termination;
     const int ai = (st.adaptive_rho && a.adaptive_interval) ? a.adaptive_interval : 0;
@@ -487,13 +495,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? M
 
         // x~ = g + sigma M^-1 x + (A^ M^-1)' (w_top - w_bot),  w = rho z - y
         const T wt = tt_fma(rho, zt, -yt) - tt_fma(rho, zb, -yb);
-        if (r < NC) {
-            bxh[r] = lr ? xs : T(0);
-            bwh[r] = lr ? wt : T(0);
+        T xi;
+        if constexpr (MERGED) {
+            const T atw = (DT * K0T) * ssum(ET * wt, lane);  // A^'(w_top - w_bot)
+            if (r < NC) bxh[r] = lr ? tt_fma(sigT, xs, atw) : T(0);
+            wave_sync();
+            xi = row_dot(Srow, bxh, gk);
+            wave_sync();
+        } else {
+            if (r < NC) {
+                bxh[r] = lr ? xs : T(0);
+                bwh[r] = lr ? wt : T(0);
+            }
+            wave_sync();
+            xi = row_dot(Srow, bxh, gk) + row_dot(Btc, bwh, T(0));
+            wave_sync();
         }
-        wave_sync();
-        const T xi = row_dot(Srow, bxh, gk) + row_dot(Btc, bwh, T(0));
-        wave_sync();
         const T xn = lr ? tt_fma(alpha, xi, oma * xs) : T(0);
         const T dx = xn - xs;
         if (!done) xs = xn;
@@ -645,7 +662,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? M
 template <typename T, int NC>
 int plant_step_launch_t(const PlantStepArgs &a, hipStream_t s)
 {
-    hipLaunchKernelGGL((plant_step_kernel<T, NC>), dim3((a.n_plants + 1) / 2), dim3(64), 0, s, a);
+    if (NC <= 20 && a.wpe == 3) hipLaunchKernelGGL((plant_step_kernel<T, NC, 3>), dim3((a.n_plants + 1) / 2), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL((plant_step_kernel<T, NC, 2>), dim3((a.n_plants + 1) / 2), dim3(64), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

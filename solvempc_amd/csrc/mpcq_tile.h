@@ -398,7 +398,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     static_assert(!PAIRED || (KM == 2 * KN && ALL_INEQ && LFREE), "paired loop: m = 2n, inequality rows, l free");
     static_assert(!MIX || (PAIRED && std::is_same<T, double>::value && !STREAM), "mixed: the fp64 paired loop");
     constexpr int VEC = 16 / sizeof(T);
-    constexpr TileLayout L = TileLayout::make(KN, KM, VEC);
+    constexpr TileLayout L = TileLayout::make(KN, KM, VEC, PAIRED);
+    // the paired loop reads the paired image set, stored after the generic one (TileLayout)
+    constexpr size_t IMG0 = PAIRED ? TileLayout::make(KN, KM, VEC, false).total : 0;
+    constexpr int KBT = L.KBT, NBS = L.NBS;  // k-steps of the Bt / AhT images; tiles of [B~; S]
     constexpr int NT = L.NT, MT = L.MT, KNP = L.KNP, KMP = L.KMP;
     constexpr int NS = 4 * NT, MS = 4 * MT;  // registers per n- / m-vector
     constexpr int NCP = 16 * NT, MCP = 16 * MT;  // padded row counts (== ctx nc, mc)
@@ -437,7 +440,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     // ---- plant images -> LDS (16 B per thread per step; every load issued before the stores)
     {
         typedef T vec __attribute__((ext_vector_type(VEC)));
-        const vec *src = (const vec *)a.img;
+        const vec *src = (const vec *)(a.img + IMG0);
         vec *dst = (vec *)img;
         constexpr int NV = (int)(L.total / VEC), PER = (NV + NTH - 1) / NTH;
         vec buf[PER];
@@ -920,7 +923,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
 #pragma unroll
             for (int k = 0; k < KNR; k++) {
                 rS[t][k] = im[L.S + TileLayout::at(KNP, VEC, t, k, ln)];
-                rBt[t][k] = im[L.Bt + TileLayout::at(KMP, VEC, t, k, ln)];
+                rBt[t][k] = im[L.Bt + TileLayout::at(KBT, VEC, t, k, ln)];
                 rB[t][k] = im[L.B + TileLayout::at(KNP, VEC, t, k, ln)];
             }
         }
@@ -1007,6 +1010,63 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                     y[gi][s] = t - zn;
                     z[gi][s] = zn;
                 }
+        }
+    };
+    // f64 paired loop (NBS > 0): piter_fast with z~ and the next S x' from ONE stacked product [B~; S] eta'
+    // (ceil(8 KN / 16) tiles instead of 2 NT: 15 f64 MFMAs instead of 20 at N = 20; a 16x16x4 f64 MFMA
+    // holds the matrix pipe 64 cycles, and the second tile of each separate product carries 4 rows).
+    // x' = eta' + (1 - alpha) x'_old, so the next -g + S x' = (1 - alpha)(-g + S x'_old) + alpha (-g) + S eta':
+    // the product's S rows start from that (a contraction by |1 - alpha| < 1: rounding does not build up).
+    constexpr int NBR = NBS > 0 ? NBS : 1;
+    auto load_regs_stk = [&](T (&rBt)[NTR][KNR], T (&rBS)[NBR][KNR]) {
+        const T *im = fresh_ptr((const T *)img);
+#pragma unroll
+        for (int t = 0; t < NTR; t++)
+#pragma unroll
+            for (int k = 0; k < KNR; k++) rBt[t][k] = im[L.Bt + TileLayout::at(KBT, VEC, t, k, lane)];
+#pragma unroll
+        for (int t = 0; t < NBR; t++)
+#pragma unroll
+            for (int k = 0; k < KNR; k++) rBS[t][k] = im[L.BS + TileLayout::at(KNP, VEC, t, k, lane)];
+    };
+    auto piter_stk = [&](const T (&rBt)[NTR][KNR], const T (&rBS)[NBR][KNR], T (&sx)[G][NS], const T (&adk)[G][KNR]) {
+        if constexpr (NBS > 0) {
+            T wt[G][KNR];
+#pragma unroll
+            for (int gi = 0; gi < G; gi++)
+#pragma unroll
+                for (int s = 0; s < KN; s++)
+                    wt[gi][s] = rho[gi] * ((z[gi][s] - y[gi][s]) - (z[gi][s + KN] - y[gi][s + KN]));
+            T xi[G][NS];
+            reg_mv<T, G, NT, KN, KNR, false, KNR>(rBt, wt, rBt, wt, xi, sx);  // xi = (-g + S x') + B~' w~
+            T ini[G][4 * NBR];  // z~ rows from 0, S rows from (1 - alpha)(-g + S x'_old) + alpha (-g)
+#pragma unroll
+            for (int gi = 0; gi < G; gi++)
+#pragma unroll
+                for (int f = 0; f < 4 * NBR; f++)
+                    ini[gi][f] = (f >= KN && f < 2 * KN) ? tt_fma(oma, sx[gi][f - KN], alpha * gv[gi][f - KN]) : T(0);
+#pragma unroll
+            for (int gi = 0; gi < G; gi++)
+#pragma unroll
+                for (int s = 0; s < KN; s++) {
+                    xi[gi][s] = adk[gi][s] * xi[gi][s];           // eta' = alpha eta
+                    xs[gi][s] = tt_fma(oma, xs[gi][s], xi[gi][s]);  // x' = alpha eta + (1 - alpha) x'
+                }
+            T out[G][4 * NBR];
+            reg_mv<T, G, NBR, KN, NS, false, KNR>(rBS, xi, rBS, wt, out, ini);  // [alpha z~_top; next -g + S x']
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+#pragma unroll
+                for (int s = 0; s < KN; s++) sx[gi][s] = out[gi][KN + s];
+#pragma unroll
+                for (int s = 0; s < KM; s++) {
+                    const T v = s < KN ? tt_fma(oma, z[gi][s], out[gi][s]) : tt_fma(oma, z[gi][s], -out[gi][s - KN]);
+                    const T t = v + y[gi][s];
+                    const T zn = vmin(t, uh[gi][s]);
+                    y[gi][s] = t - zn;
+                    z[gi][s] = zn;
+                }
+            }
         }
     };
     // piter_fast's f32 arithmetic on packed pairs (v_pk_fma/add/mul_f32: two elements per VALU issue,
@@ -1192,7 +1252,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
 #pragma unroll
                             for (int k = 0; k < KNR; k++) {
                                 rS32[t][k] = (float)im[L.S + TileLayout::at(KNP, VEC, t, k, ln)];
-                                rBt32[t][k] = (float)im[L.Bt + TileLayout::at(KMP, VEC, t, k, ln)];
+                                rBt32[t][k] = (float)im[L.Bt + TileLayout::at(KBT, VEC, t, k, ln)];
                                 rB32[t][k] = (float)im[L.B + TileLayout::at(KNP, VEC, t, k, ln)];
                             }
                         }
@@ -1218,7 +1278,29 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 if (a.stamps) info_cycles += (long long)__builtin_amdgcn_s_memtime() - t_mix;
 #endif
             }
-            if (it + 1 < nxt) {
+            if constexpr (NBS > 0) {
+                if (it + 1 < nxt) {
+                    T rBt[NTR][KNR], rBS[NBR][KNR];
+                    load_regs_stk(rBt, rBS);
+                    T sx[G][NS], adk[G][KNR];
+                    tile_mv_g<T, G, NT, KN, KNP>(img + L.S, xs, sx, lane, gv);  // -g + S x'
+#pragma unroll
+                    for (int gi = 0; gi < G; gi++) {
+#pragma unroll
+                        for (int s = 0; s < KN; s++) adk[gi][s] = alpha * dk[gi][s];
+#pragma unroll
+                        for (int s = 0; s < KM; s++) y[gi][s] = y[gi][s] * rinv[gi];  // y -> yt = y / rho
+                    }
+                    do {
+                        it++;
+                        piter_stk(rBt, rBS, sx, adk);
+                    } while (it + 1 < nxt);
+#pragma unroll
+                    for (int gi = 0; gi < G; gi++)
+#pragma unroll
+                        for (int s = 0; s < KM; s++) y[gi][s] = y[gi][s] * rho[gi];  // yt -> y
+                }
+            } else if (it + 1 < nxt) {
                 T rS[NTR][KNR], rBt[NTR][KNR], rB[NTR][KNR];
                 load_regs(rS, rBt, rB);
                 T sx[G][NS], adk[G][KNR];
@@ -1293,8 +1375,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 T rS[NTR][KNR], rBt[NTR][KNR], rB[NTR][KNR];
                 load_regs(rS, rBt, rB);
                 piter(with_delta, rS, rBt, rB);
-                return;
-            }
+            } else {
             // xi = -g + sigma W'W x' + B' w,   w_j = rho_j z_j - y_j   (w reuses the zt registers)
             T wz[G][MS];
 #pragma unroll
@@ -1337,6 +1418,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                     y[gi][s] = tt_fma(rj, v - zn, y[gi][s]);
                     z[gi][s] = zn;
                 }
+            }
         };
         if (!info) {
             iterate(std::false_type{});
@@ -1405,7 +1487,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 for (int gi = 0; gi < G; gi++)
 #pragma unroll
                     for (int s = 0; s < KN; s++) yd[gi][s] = y[gi][s] - y[gi][s + KN];
-                tile_mv_g<T, G, NT, KN, KMP, KNR, REM4>(img + L.AhT, yd, aty, lane, nullptr);
+                tile_mv_g<T, G, NT, KN, KBT, KNR, REM4>(img + L.AhT, yd, aty, lane, nullptr);
             } else {
                 tile_mv_g<T, G, NT, KM, KMP>(img + L.AhT, y, aty, lane, nullptr);
             }
@@ -1498,7 +1580,16 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             }
             if (!wave_any(anyc)) return;
             T atd[G][NS];
-            tile_mv_g<T, G, NT, KM, KMP>(img + L.AhT, d, atd, lane, nullptr);
+            if constexpr (PAIRED) {  // A' d = A~' (d_top - d_bot)
+                T dd[G][KNR];
+#pragma unroll
+                for (int gi = 0; gi < G; gi++)
+#pragma unroll
+                    for (int s = 0; s < KN; s++) dd[gi][s] = d[gi][s] - d[gi][s + KN];
+                tile_mv_g<T, G, NT, KN, KBT, KNR, REM4>(img + L.AhT, dd, atd, lane, nullptr);
+            } else {
+                tile_mv_g<T, G, NT, KM, KMP>(img + L.AhT, d, atd, lane, nullptr);
+            }
             const T *Dinv = fresh_ptr((const T *)s_Dinv);
 #pragma unroll
             for (int gi = 0; gi < G; gi++) {
@@ -1558,7 +1649,17 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             }
             if (!wave_any(anyc)) return;
             T adx[G][MS];
-            tile_mv_g<T, G, MT, KN, KNP>(img + L.B, dx, adx, lane, nullptr);
+            if constexpr (PAIRED) {  // A dx: the top rows B~ dx', the bottom ones their negation
+                T adt[G][NS];
+                tile_mv_g<T, G, NT, KN, KNP, NS, REM4>(img + L.B, dx, adt, lane, nullptr);
+#pragma unroll
+                for (int gi = 0; gi < G; gi++)
+#pragma unroll
+                    for (int s = 0; s < MS; s++)
+                        adx[gi][s] = s < KN ? adt[gi][s] : (s < KM ? -adt[gi][s < KM ? s - KN : 0] : T(0));
+            } else {
+                tile_mv_g<T, G, MT, KN, KNP>(img + L.B, dx, adx, lane, nullptr);
+            }
             const T *Einv = fresh_ptr((const T *)s_Einv);
 #pragma unroll
             for (int gi = 0; gi < G; gi++) {
