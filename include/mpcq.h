@@ -54,7 +54,7 @@ extern "C" {
                             iterations before the last MPCQ_MIX_R of every check interval run in fp32
                             (MFMA f32 products), which the fp64 ones damp; every
                             other path is MPCQ_F64                                               */
-#define MPCQ_MIX_R 8
+#define MPCQ_MIX_R 5
 
 /* OSQP v0.6 settings (osqp constants.h defaults via mpcq_default_settings).  Replaces
  * OsqpEigen::Settings as used at ModelPredictiveControlAPI.cpp:51-52 (setVerbosity,

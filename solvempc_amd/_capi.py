@@ -10,7 +10,7 @@ SOLVED, SOLVED_INACCURATE, PRIMAL_INFEASIBLE_INACCURATE, DUAL_INFEASIBLE_INACCUR
 MAX_ITER_REACHED, PRIMAL_INFEASIBLE, DUAL_INFEASIBLE, NON_CVX, UNSOLVED = -2, -3, -4, -7, -10
 INVALID_BOUNDS, TYPE_CHANGED = -20, -21
 MPCQ_F64, MPCQ_F32, MPCQ_F64_MIXED = 0, 1, 2
-MPCQ_MIX_R = 8  # include/mpcq.h: fp64 iterations per check interval of MPCQ_F64_MIXED
+MPCQ_MIX_R = 5  # include/mpcq.h: fp64 iterations per check interval of MPCQ_F64_MIXED
 
 # Every symbol include/mpcq.h declares (tests check the library exports all of them).
 EXPORTS = (

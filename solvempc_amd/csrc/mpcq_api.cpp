@@ -50,7 +50,7 @@ constexpr int kMaxPhases = 16;
 //   MPCQ_TAIL=wave|tile         the tile chain's last launch on the one-QP-per-wave / tile kernel
 //   MPCQ_MIX_R=r                MPCQ_F64_MIXED: fp64 iterations per check interval (default MPCQ_MIX_R)
 //   MPCQ_TILE_OCC=2|3           waves per SIMD of the f32 paired tile kernel (default 3)
-//   MPCQ_PLANT_WPE=2|3          waves per SIMD of the one-pass per-plant kernel (default 2)
+//   MPCQ_PLANT_WPE=2|3          waves per SIMD of the one-pass per-plant kernel (default f64 3, f32 2)
 // Debug builds (-DMPCQ_DEBUG_HOOKS) add the stamp / profiling dumps (MPCQ_TILE_STAMPS,
 // MPCQ_SETUP_PROF, MPCQ_MIMO_SETUP_STAMPS, MPCQ_MIMO_STAMPS) and MPCQ_DEBUG_SYNC.
 const char *test_hook(const char *name)
@@ -1533,8 +1533,10 @@ int mpcq_mpc_plants_step_device(mpcq_ctx *c, int nx, int s_rows, const double *A
     a.x = c->d_x; a.y = c->d_y; a.rho_out = c->d_rho; a.status = c->d_status; a.iter = c->d_iter;
     a.flags = c->d_flags;
     {
-        const char *w = test_hook("MPCQ_PLANT_WPE");  // (A/B: the 3-waves/SIMD variant)
-        a.wpe = *w ? std::atoi(w) : 2;
+        // fp64 at 3 waves/SIMD (189 -> 168 VGPRs, a few spills in the check code: 39.4-40.0 M QP/s against
+        // 35.5-35.9 M at 2), fp32 at 2 (3 spills into its loop: slower); MPCQ_PLANT_WPE=2|3 for A/B
+        const char *w = test_hook("MPCQ_PLANT_WPE");
+        a.wpe = *w ? std::atoi(w) : (c->dims.dtype == MPCQ_F32 ? 2 : 3);
     }
     const int lr = mpcq_internal_plant_step_launch(&a, c->dims.dtype == MPCQ_F32, s);
     if (lr) return fail(lr == -1 ? MPCQ_ERR_ARG : MPCQ_ERR_HIP, "plants_step kernel launch failed");
