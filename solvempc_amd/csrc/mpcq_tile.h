@@ -427,55 +427,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
         if (a.zero_cnt0) a.zero_cnt0[threadIdx.x * ListSeg::kStride] = 0;
     }
     if (blk * (refill ? WPB * a.sim.cpw : QPW) >= count) return;  // whole workgroup idle in this phase (uniform)
-    // this wave's 16 G QPs: slots wave_slot.. of the launch's list (or of the batch in phase 0); a
-    // stream wave holds a.sim.cpw plants in its first columns.  Assigned here, and (PF: not a stream) the
-    // per-QP inputs the prologue reads first (X, U; a resumed or warm phase's x', z, y, rho) loaded here,
-    // so that their latency overlaps the image copy below instead of following it.
-    constexpr bool PF = !STREAM;
-    constexpr int NSX = 4 * L.NT, MSX = 4 * L.MT;
-    const int cpw = refill ? a.sim.cpw : 16 * G;
-    const int wave_slot = (blk * WPB + (threadIdx.x >> 6)) * cpw;
-    const bool wave_on = wave_slot < count;
-    bool valid0[G];
-    int bq0[G];
-#pragma unroll
-    for (int gi = 0; gi < G; gi++) {
-        const int slot = wave_slot + 16 * gi + (threadIdx.x & 15);
-        valid0[gi] = slot < count && (!refill || (int)(threadIdx.x & 15) < cpw);
-        const int i = slot + (seglist ? seg * a.list_seg : 0);  // list entry
-        bq0[gi] = valid0[gi] ? (seglist ? a.list_in[i] : a.qp0 + i) : 0;
-    }
-    const bool pf_state = a.resume != 0 || (a.warm && !a.fresh);  // the first load_cols reads the saved state
-    double pfX[G][8], pfU[G];
-    T pfx[G][PF ? NSX : 1], pfz[G][PF ? MSX : 1], pfy[G][PF ? MSX : 1], pfrho[G];
-    int pfit = 0;
-    if (PF && wave_on) {
-        const int gq = (int)(threadIdx.x >> 4) & 3;
-#pragma unroll
-        for (int gi = 0; gi < G; gi++) {
-            const int b = bq0[gi];
-            if (a.X != nullptr) {
-                const int nx = a.nx;
-#pragma unroll
-                for (int t = 0; t < 8; t++) pfX[gi][t] = a.X[(size_t)b * nx + (t < nx ? t : 0)];
-#pragma unroll
-                for (int t = 0; t < 8; t++)
-                    if (t >= nx) pfX[gi][t] = 0.0;
-                pfU[gi] = a.U[b];
-            }
-            if (a.resume || !a.fresh) pfrho[gi] = a.rhos[b];
-            if (gi == 0 && a.resume) pfit = a.it_state[b];
-            if (pf_state) {
-#pragma unroll
-                for (int s = 0; s < NSX; s++) pfx[gi][s] = s < KN ? a.xs[(size_t)b * (16 * L.NT) + 4 * s + gq] : T(0);
-#pragma unroll
-                for (int s = 0; s < MSX; s++) {
-                    pfz[gi][s] = s < KM ? a.zs[(size_t)b * (16 * L.MT) + 4 * s + gq] : T(0);
-                    pfy[gi][s] = s < KM ? a.ys[(size_t)b * (16 * L.MT) + 4 * s + gq] : T(0);
-                }
-            }
-        }
-    }
     for (int i = threadIdx.x; i < NCP; i += NTH) {
         s_lam[i] = a.ops.lam[i];
         s_D[i] = a.ops.D[i];
@@ -557,6 +508,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
 #define MPCQ_PRO_MARK(k) do { } while (0)
 #endif
 
+    const int lane = threadIdx.x & 63, c = lane & 15;
     constexpr int KNR = PAIRED ? KN : 1, NTR = PAIRED ? NT : 1;
     // f32 paired loop with n = 16 (NT - 1) + 4 (N = 20): the last tile's 4 rows on the 4x4x1 MFMA
     constexpr bool REM4F = PAIRED && KN % 4 == 1 && NT > 1 && MPCQ_REM4;  // (the fp32 loop's remainder tile)
@@ -626,10 +578,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
 #pragma unroll
                 for (int t = 0; t < 8; t++) Xv[t] = sX[t];
                 Uv = sU;
-            } else if (PF && entry) {
-#pragma unroll
-                for (int t = 0; t < 8; t++) Xv[t] = pfX[gi][t];
-                Uv = pfU[gi];
             } else {
 #pragma unroll
                 for (int t = 0; t < 8; t++) Xv[t] = a.X[(size_t)b * nx + (t < nx ? t : 0)];
@@ -766,21 +714,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             continue;
         }
         const int b = b_[gi];
-        if constexpr (PF) {  // (entry: the values loaded before the image copy)
-            if (resume) {
-                rho[gi] = pfrho[gi];
-                if (gi == 0) it = pfit;
-            } else {
-                rho[gi] = fresh ? (T)fmin(fmax(st.rho, kRhoMin), kRhoMax) : pfrho[gi];
-            }
-#pragma unroll
-            for (int s = 0; s < NS; s++) xs[gi][s] = (load_state && s < KN) ? pfx[gi][s] : T(0);
-#pragma unroll
-            for (int s = 0; s < MS; s++) {
-                z[gi][s] = (load_state && s < KM) ? pfz[gi][s] : T(0);
-                y[gi][s] = (load_state && s < KM) ? pfy[gi][s] : T(0);
-            }
-        } else {
         if (resume) {
             rho[gi] = a.rhos[b];
             if (gi == 0) it = a.it_state[b];
@@ -793,7 +726,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
         for (int s = 0; s < MS; s++) {
             z[gi][s] = (load_state && s < KM) ? a.zs[(size_t)b * mcs + 4 * s + g] : T(0);
             y[gi][s] = (load_state && s < KM) ? a.ys[(size_t)b * mcs + 4 * s + g] : T(0);
-        }
         }
         rinv[gi] = T(1) / rho[gi];
         cst[gi] = it;
@@ -1895,7 +1827,22 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
 #endif
     };  // run_group
 
-    if (wave_on) run_group(bq0, valid0);
+    // this wave's 16 G QPs: slots wave_slot.. of the launch's list (or of the batch in phase 0); a
+    // stream wave holds a.sim.cpw plants in its first columns
+    const int cpw = refill ? a.sim.cpw : 16 * G;
+    const int wave_slot = (blk * WPB + (threadIdx.x >> 6)) * cpw;
+    if (wave_slot < count) {
+        bool valid[G];
+        int b_[G];
+#pragma unroll
+        for (int gi = 0; gi < G; gi++) {
+            const int slot = wave_slot + 16 * gi + c;
+            valid[gi] = slot < count && (!refill || c < cpw);
+            const int i = slot + (seglist ? seg * a.list_seg : 0);  // list entry
+            b_[gi] = valid[gi] ? (seglist ? a.list_in[i] : a.qp0 + i) : 0;
+        }
+        run_group(b_, valid);
+    }
     MPCQ_TSTAMP(4, (long long)__builtin_amdgcn_s_memtime());
     MPCQ_TSTAMP(7, (long long)__builtin_amdgcn_s_memrealtime());
 }
