@@ -46,8 +46,8 @@ def parse(argv=None):
     p.add_argument("--horizon", type=int, default=20)
     p.add_argument("--dtype", choices=("f64", "f32", "mixed"), default=None,
                    help="ADMM arithmetic (default: the fastest path inside north_star's 1e-5 on the applied move: "
-                        "mixed for cfg2, f64 for perplant (its fp32 ADMM misses it, at ~8%% less time); f32 for "
-                        "the stream; quadrotor is f64)")
+                        "mixed for cfg2 and the stream, f64 for perplant (faster than its fp32 kernel, which misses "
+                        "it); quadrotor is f64)")
     p.add_argument("--variants", type=int, default=1,
                    help="cfg2: also time the f32 and f64 paths on the same batch (the line's `variants` block)")
     p.add_argument("--seed", type=int, default=1)
@@ -72,7 +72,7 @@ def parse(argv=None):
                    help="no device: launcher, rendezvous and the gather only (CPU tests of the N > 1 plumbing)")
     a = p.parse_args(argv)
     if a.dtype is None:  # the fastest path inside north_star's 1e-5 on the applied move
-        a.dtype = {"cfg2": "mixed", "perplant": "f64"}.get(a.workload, "f32")
+        a.dtype = {"cfg2": "mixed", "perplant": "f64", "stream": "mixed"}.get(a.workload, "f32")
     if a.workload == "stream" and a.batch == 65536:
         a.batch = 4096
     if a.workload == "perplant" and a.batch == 65536:
@@ -583,6 +583,11 @@ def main_lti(a, rank, world, local, dist, dev):
         if kind == "tile" and not stream_mode and not perplant:
             f64s, f32s = workload.flops_split_mixed(N, 2 * N, 4, iters, sm.MPCQ_MIX_R, paired=paired)
             split = (float(f64s.sum()), float(f32s.sum()))
+        elif stream_mode and solver.stream_path() == "tile":  # (the tile stream mode runs the mixed loop)
+            f64s, f32s = workload.flops_split_mixed_total(N, 2 * N, 4, it_total, a.ctrl_steps, sm.MPCQ_MIX_R,
+                                                          paired=paired)
+            split = (float(f64s.sum()), float(f32s.sum()))
+        if split:
             peak = (split[0] + split[1]) / (split[0] / PEAK_TFLOPS["f64"] + split[1] / PEAK_TFLOPS["f32"])
         else:  # (every other path runs MPCQ_F64_MIXED in fp64)
             peak = PEAK_TFLOPS["f64"]
@@ -626,16 +631,19 @@ def main_lti(a, rank, world, local, dist, dev):
         # a refactorisation per plant whose rho moved), priced at the vector peak of the ADMM's type.
         rho0 = solver.settings.rho if a.dtype != "f32" else float(np.float32(solver.settings.rho))
         refac = (rho_f != rho0).astype(np.float64)
-        pf = float(workload.flops_plant_step(N, 4, iters, refac, solver.settings.scaling).sum())
+        merged = a.dtype != "f32"  # (the fp64 kernel's one-GEMV iteration, mpcq_plant.hip)
+        pf = float(workload.flops_plant_step(N, 4, iters, refac, solver.settings.scaling, merged=merged).sum())
         ach = pf / (kern_ms * 1e-3) / 1e12
         rec["roofline"] = {"bound": "valu", "achieved": ach, "peak": peak, "unit": "TFLOP/s",
                            "frac": ach / peak, "traffic": None,
                            "kernel": "plant_step_kernel (condense + setup + solve, one pass)", "kernel_ms": kern_ms,
                            "flops_per_step": pf,
                            "flops_note": "as performed (workload.flops_plant_step): condensing by lag scans, Ruiz, "
-                                         "2N^3 + 10N^2 per KKT inverse (setup + one per rho change), 4N^2 + 23N per "
-                                         "iteration (A structural: prefix / suffix scans), 2N^2 + 36N per check; the "
-                                         "fp64 setup is priced at the same peak",
+                                         + ("2N^3 + 6N^2 per KKT inverse (setup + one per rho change), 2N^2 + 28N per "
+                                            "iteration (one GEMV, A^'w and A^x by suffix / prefix scans)" if merged else
+                                            "2N^3 + 10N^2 per KKT inverse (setup + one per rho change), 4N^2 + 23N per "
+                                            "iteration (A structural: prefix / suffix scans)")
+                                         + ", 2N^2 + 36N per check; the fp64 setup is priced at the same peak",
                            "dense_equivalent": {"flops_per_step": flops_dense + B * workload.flops_plant_setup(N, 2 * N),
                                                 "note": "SURVEY §8d: dense F_iter / F_check + F_condense + Ruiz + one LDL"}}
         rec["iters"]["rho_adapted_frac"] = float(refac.mean())

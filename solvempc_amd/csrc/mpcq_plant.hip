@@ -69,16 +69,21 @@ __device__ inline double limit_scaling_p(double d)
     return d > kMaxScaling ? kMaxScaling : d;
 }
 
-// DPP move whose lanes without a source (row shifts) or outside the row mask RM read 0
+// DPP move whose lanes without a source (row shifts) or outside the row mask RM read 0.  With every row
+// enabled the zero comes from bound_ctrl (no old value: no zeroing move before each DPP move).
+template <int CTRL, int RM> __device__ __forceinline__ unsigned dpp0_u(unsigned v)
+{
+    if constexpr (RM == 0xF) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+    else return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, 0xF, false);
+}
 template <int CTRL, int RM = 0xF> __device__ __forceinline__ float dpp0(float v)
 {
-    return __uint_as_float((unsigned)__builtin_amdgcn_update_dpp(0, (int)__float_as_uint(v), CTRL, RM, 0xF, false));
+    return __uint_as_float(dpp0_u<CTRL, RM>(__float_as_uint(v)));
 }
 template <int CTRL, int RM = 0xF> __device__ __forceinline__ double dpp0(double v)
 {
     const unsigned long long u = (unsigned long long)__double_as_longlong(v);
-    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, RM, 0xF, false);
-    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, RM, 0xF, false);
+    const unsigned lo = dpp0_u<CTRL, RM>((unsigned)u), hi = dpp0_u<CTRL, RM>((unsigned)(u >> 32));
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 __device__ __forceinline__ float readlane_t(float v, int l)
@@ -428,7 +433,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     double rho_f = rho0;
     const T alpha = (T)st.alpha, oma = T(1) - (T)st.alpha;
     const T ET = (T)(lr ? Er : 0.0), DT = (T)Dd, K0T = (T)K0;
-    const T EK = ET * K0T;  // (A^ x)_r = E_r K0 sum_{k<=r} D_k x_k
+    // (A^ x)_r = E_r K0 sum_{k<=r} D_k x_k: E_r K0 is formed in the loop from ET, K0T (one multiply,
+    // where a hoisted copy was the 3-waves/SIMD allocation's spill reloaded every iteration)
     const T sigT = (T)st.sigma;
     const bool scaled_term = st.scaled_termination != 0;
     const int ct = st.check_termination;
@@ -515,7 +521,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         const T dx = xn - xs;
         if (!done) xs = xn;
         // z~ = A^ x~ (top rows; bottom = -top), relaxation, projection onto [l, u], dual update
-        const T zz = EK * psum(DT * xi);
+        T ETl = ET;
+        asm volatile("" : "+v"(ETl));
+        const T zz = (ETl * K0T) * psum(DT * xi);
         T dyt = T(0), dyb = T(0);
         if (lr && !done) {
             T v = tt_fma(alpha, zz, oma * zt);

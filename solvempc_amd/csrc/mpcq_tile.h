@@ -396,7 +396,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     MPCQ_TSTAMP(0, (long long)__builtin_amdgcn_s_memtime());
     MPCQ_TSTAMP(6, (long long)__builtin_amdgcn_s_memrealtime());
     static_assert(!PAIRED || (KM == 2 * KN && ALL_INEQ && LFREE), "paired loop: m = 2n, inequality rows, l free");
-    static_assert(!MIX || (PAIRED && std::is_same<T, double>::value && !STREAM), "mixed: the fp64 paired loop");
+    static_assert(!MIX || (PAIRED && std::is_same<T, double>::value), "mixed: the fp64 paired loop");
     constexpr int VEC = 16 / sizeof(T);
     constexpr TileLayout L = TileLayout::make(KN, KM, VEC, PAIRED);
     // the paired loop reads the paired image set, stored after the generic one (TileLayout)
@@ -1869,6 +1869,13 @@ int tile_stream_launch(const AdmmArgs<T> &a, hipStream_t s)
         if (a.paired && a.all_ineq && a.lower_free) {
             constexpr int OCC = 2, WPB = 4;  // (a stream is latency-bound: few waves, no spills)
             const int waves = (a.batch + a.sim.cpw - 1) / a.sim.cpw;
+            if constexpr (std::is_same<T, double>::value) {
+                if (a.mix_r > 0) {  // MPCQ_F64_MIXED: each step's plain iterations before the last mix_r in fp32
+                    hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 1, OCC, true, WPB, true, true>),
+                                       dim3((waves + WPB - 1) / WPB), dim3(64 * WPB), 0, s, a);
+                    return hipGetLastError() == hipSuccess ? 0 : -2;
+                }
+            }
             hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 1, OCC, true, WPB, true>),
                                dim3((waves + WPB - 1) / WPB), dim3(64 * WPB), 0, s, a);
             return hipGetLastError() == hipSuccess ? 0 : -2;

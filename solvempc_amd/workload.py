@@ -180,6 +180,22 @@ def flops_per_qp_total(n: int, m: int, nx: int, iters_total, solves: int, check:
     return it * f_iter + np.floor(it / check) * f_check + solves * f_front
 
 
+def flops_split_mixed_total(n: int, m: int, nx: int, iters_total, solves: int, mix_r: int, check: int = 25,
+                            paired: bool = False) -> tuple[np.ndarray, np.ndarray]:
+    """flops_per_qp_total of an MPCQ_F64_MIXED stream split into (fp64, fp32): every solve of the stream
+    stops on a check iteration, so each of its floor(total / check) intervals runs mix_r iterations
+    (the last ones: damping and the info iteration) and its check in fp64, the rest in fp32; the front
+    ends are fp64."""
+    it = np.asarray(iters_total, dtype=np.int64)
+    f_iter, f_check, f_front = _flop_terms(n, m, nx, paired)
+    r = min(max(int(mix_r), 1), check)
+    full = it // check
+    n64 = full * r + np.maximum(it % check - (check - r), 0)
+    f64 = n64 * float(f_iter) + full * float(f_check) + solves * float(f_front)
+    f32 = (it - n64) * float(f_iter)
+    return f64.astype(np.float64), f32.astype(np.float64)
+
+
 def flops_plant_setup(n: int, m: int, N: int | None = None) -> float:
     """Algorithmic FLOPs of one plant's condensing + setup: F_condense (SISO)
     4N^3 + 10N^2 + 128N, Ruiz 10*3(n^2 + nm), F_setup 2n^2 m + n^3/3 + n^2 (one LDL of the KKT
@@ -188,7 +204,8 @@ def flops_plant_setup(n: int, m: int, N: int | None = None) -> float:
     return (4 * N ** 3 + 10 * N ** 2 + 128 * N) + 30 * (n * n + n * m) + (2 * n * n * m + n ** 3 / 3 + n * n)
 
 
-def flops_plant_step(N: int, nx: int, iters, refactors, scaling: int = 10, check: int = 25) -> np.ndarray:
+def flops_plant_step(N: int, nx: int, iters, refactors, scaling: int = 10, check: int = 25,
+                     merged: bool = False) -> np.ndarray:
     """FLOPs plant_step_kernel performs per plant (mpcq_plant.hip; FMA = 2, m = 2N with the paired rows,
     A = [K0 L; -K0 L] applied structurally):
     * condensing: the Ad^k Bd / Cd Ad^k recurrences 4 N nx^2, CAB and the free response 4 N nx, the
@@ -198,13 +215,16 @@ def flops_plant_step(N: int, nx: int, iters, refactors, scaling: int = 10, check
       2 N^2, the (A^ M^-1) columns by prefix sums 4 N^2;
     * front end 2 N (nx + 2);
     * per iteration: sigma M^-1 x and (A^ M^-1)' w, 4 N^2, the A^ x~ prefix scan ~3 N, ~20 N element-wise;
-    * per check: P^ x 2 N^2, the A^ x and A^'y scans ~6 N, ~30 N of residuals and norms (fp64)."""
+    * per check: P^ x 2 N^2, the A^ x and A^'y scans ~6 N, ~30 N of residuals and norms (fp64).
+    merged (the fp64 kernel): one GEMV per iteration, M^-1 (sigma x + A^'w) with A^'w a suffix scan: 2 N^2
+    + ~28 N per iteration, and no (A^ M^-1) columns per factorisation."""
     it = np.asarray(iters, dtype=np.float64)
     cond = 4 * N * nx * nx + 4 * N * nx + 6 * N * N
     ruiz = scaling * (4 * N * N + 4 * N)
-    kkt = 2 * N ** 3 + 10 * N * N
+    kkt = 2 * N ** 3 + (6 if merged else 10) * N * N
+    per_it = 2 * N * N + 28 * N if merged else 4 * N * N + 23 * N
     return (cond + ruiz + 2 * N * (nx + 2) + (1 + np.asarray(refactors, dtype=np.float64)) * kkt
-            + it * (4 * N * N + 23 * N) + np.floor(it / check) * (2 * N * N + 36 * N))
+            + it * per_it + np.floor(it / check) * (2 * N * N + 36 * N))
 
 
 # ----------------------------------------------------------------------------- config 4: quad-rotor

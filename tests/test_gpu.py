@@ -586,7 +586,7 @@ def test_receding_horizon_stream_f32(plant, kernel):
 
 
 @pytest.mark.parametrize("family", ["tile", "wave"])
-@pytest.mark.parametrize("dtype", ["f32", "f64"])
+@pytest.mark.parametrize("dtype", ["f32", "f64", "mixed"])
 def test_stream_one_launch_matches_graph(plant, dtype, family, monkeypatch):
     """mpcq_mpc_run_device's one-launch stream against the per-step hipGraph path (MPCQ_STREAM=graph) of
     the same kernel family, from the same cold state: the tile kernel's stream mode (every MFMA column
@@ -730,7 +730,7 @@ def test_stream_workload_stays_solved_and_bounded(plant):
     assert np.abs(Xd.cpu().numpy()).max() < 10 and np.abs(Ud.cpu().numpy()).max() < 10
 
 
-@pytest.mark.parametrize("dtype", ["f32", "f64"])
+@pytest.mark.parametrize("dtype", ["f32", "f64", "mixed"])
 def test_stream_bench_path_matches_oracle(plant, dtype, monkeypatch):
     """The config-5 bench path itself (one tile-stream launch, 4 plants per wave as the bench's 4,096-plant
     batch runs it) at 512 plants x 1,000 warm-started control steps against oracle.stream_run (one
@@ -738,7 +738,9 @@ def test_stream_bench_path_matches_oracle(plant, dtype, monkeypatch):
     SOLVED on both sides; fp64: every plant's iteration total equal and the final U within 1e-8; fp32
     (the bench's dtype, whose closed loops drift from the fp64 ones by rounding over 1,000 steps): the
     iteration totals equal on >= 99 % of plants (the rest: an fp32 schedule tie somewhere in the 1,000
-    steps, within 1 % of the total) and the final U within 1e-3."""
+    steps, within 1 % of the total) and the final U within 1e-3; mixed (the tile stream mode with each step's
+    plain iterations before the last MPCQ_MIX_R in fp32): totals equal on >= 99 % of plants and the final U
+    within north_star's 1e-5 after the 1,000 closed-loop steps."""
     import torch
     monkeypatch.setenv("MPCQ_STREAM_CPW", "4")
     N, B, steps, seed, noise = 20, 512, 1000, 4, 1e-2
@@ -766,7 +768,7 @@ def test_stream_bench_path_matches_oracle(plant, dtype, monkeypatch):
     else:
         assert same.mean() >= 0.99, same.mean()
         assert (np.abs(it_dev - itc) / itc).max() < 0.01
-        assert dU.max() < 1e-3, dU.max()
+        assert dU.max() < (1e-5 if dtype == "mixed" else 1e-3), dU.max()
     print(f"stream {dtype}: {B} plants x {steps} steps, iteration totals equal on {same.mean():.4f}, "
           f"max |dU| {dU.max():.2e}")
 
