@@ -46,8 +46,9 @@ def parse(argv=None):
     p.add_argument("--horizon", type=int, default=20)
     p.add_argument("--dtype", choices=("f64", "f32", "mixed"), default=None,
                    help="ADMM arithmetic (default: the fastest path inside north_star's 1e-5 on the applied move: "
-                        "mixed for cfg2 and the stream, f64 for perplant (faster than its fp32 kernel, which misses "
-                        "it); quadrotor is f64)")
+                        "mixed for cfg2, f64 for perplant (faster than its fp32 kernel, which misses it) and for the "
+                        "stream (whose mixed / f32 closed loops drift up to ~3e-5 from the oracle's over 1,000 "
+                        "steps); quadrotor is f64)")
     p.add_argument("--variants", type=int, default=1,
                    help="cfg2: also time the f32 and f64 paths on the same batch (the line's `variants` block)")
     p.add_argument("--seed", type=int, default=1)
@@ -72,7 +73,7 @@ def parse(argv=None):
                    help="no device: launcher, rendezvous and the gather only (CPU tests of the N > 1 plumbing)")
     a = p.parse_args(argv)
     if a.dtype is None:  # the fastest path inside north_star's 1e-5 on the applied move
-        a.dtype = {"cfg2": "mixed", "perplant": "f64", "stream": "mixed"}.get(a.workload, "f32")
+        a.dtype = {"cfg2": "mixed", "perplant": "f64", "stream": "f64"}.get(a.workload, "f32")
     if a.workload == "stream" and a.batch == 65536:
         a.batch = 4096
     if a.workload == "perplant" and a.batch == 65536:
