@@ -215,14 +215,10 @@ struct AdmmArgs {
 // k-steps, NT tiles), plus for f64 (VEC 2) BS = [B~; S] stacked (B~ rows 0 .. 4 KN - 1, then S): the
 // plain iteration's z~ = B~ eta' and S eta' in one product (ceil(8 KN / 16) tiles instead of 2 NT).
 // The buffer holds the generic set (make(.., false)) followed by the paired one (make(.., true)).
-// W and W' come last: the kernel keeps [0, W) in LDS and reads W, W' (the prologue's W'q^, the
-// finalize's W x', the dual certificate's W dx: once per launch or per finalize) from the global copy,
-// which keeps a workgroup's LDS within a third of the CU's (tile kernel: a new workgroup can start as
-// soon as waves of the resident ones have finished, not only when a whole workgroup has).
 struct TileLayout {
     int KN, KM, NT, MT, VEC, KNP, KMP, KBT, NBS;
     bool paired;
-    size_t S, Bt, B, PW, AhT, BS, W, Wt, total;
+    size_t S, Bt, B, PW, AhT, W, Wt, BS, total;
     __host__ __device__ static constexpr TileLayout make(int KN, int KM, int VEC, bool paired = false)
     {
         TileLayout L{};
@@ -238,9 +234,9 @@ struct TileLayout {
         L.B = o;   o += (size_t)BT * L.KNP * 64;     // B = A^ W        (m x n; paired n x n)
         L.PW = o;  o += (size_t)L.NT * L.KNP * 64;   // P^ W            (n x n)
         L.AhT = o; o += (size_t)L.NT * L.KBT * 64;   // A^'             (n x m; paired n x n)
-        L.BS = o;  o += (size_t)L.NBS * L.KNP * 64;  // [B~; S]         (8 KN x n; paired f64 only)
         L.W = o;   o += (size_t)L.NT * L.KNP * 64;   // W               (n x n)
         L.Wt = o;  o += (size_t)L.NT * L.KNP * 64;   // W'              (n x n)
+        L.BS = o;  o += (size_t)L.NBS * L.KNP * 64;  // [B~; S]         (8 KN x n; paired f64 only)
         L.total = o;
         return L;
     }

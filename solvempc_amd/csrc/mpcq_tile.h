@@ -407,8 +407,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     constexpr int NCP = 16 * NT, MCP = 16 * MT;  // padded row counts (== ctx nc, mc)
     constexpr int NTH = 64 * WPB;                // threads per workgroup
     constexpr int QPW = 16 * G * WPB;            // QPs per workgroup
-    __shared__ __attribute__((aligned(16))) T img[L.W];  // [0, W): W and W' are read from gimg (TileLayout)
-    const T *const gimg = a.img + IMG0;
+    __shared__ __attribute__((aligned(16))) T img[L.total];
     __shared__ T rowv[3 * NCP + 2 * MCP];        // lam, D, Dinv | E, Einv of the plant
     // q^ of each wave's QPs (lane layout): the dual residual of every check iteration reads it here
     // instead of re-reading q (fp64, HBM) under the latency of a loaded memory system
@@ -443,7 +442,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
         typedef T vec __attribute__((ext_vector_type(VEC)));
         const vec *src = (const vec *)(a.img + IMG0);
         vec *dst = (vec *)img;
-        constexpr int NV = (int)(L.W / VEC), PER = (NV + NTH - 1) / NTH;
+        constexpr int NV = (int)(L.total / VEC), PER = (NV + NTH - 1) / NTH;
         vec buf[PER];
 #pragma unroll
         for (int k = 0; k < PER; k++) {
@@ -456,16 +455,27 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             if (i < NV) dst[i] = buf[k];
         }
     }
-    // ---- MPC front-end vectors of the plant (setF :372-375, setUpperBound :360-369) -> LDS, fp64; frr =
-    // Fr (xref 1) summed per row in the reference's order.  (Fx and Sbar rows are read from global memory
-    // by the prologue, D and E from rowv: the workgroup's LDS stays within a third of the CU's.)
-    constexpr int FE_FU = 0, FE_FR = NCP, FE_KU = 2 * NCP, FE_W0 = 2 * NCP + MCP, FE_TOT = 2 * NCP + 2 * MCP;
+    // ---- MPC front-end operators of the plant (setF :372-375, setUpperBound :360-369) -> LDS, fp64:
+    // Fx, Sbar rows padded to 8 columns; frr = Fr (xref 1) summed per row in the reference's order.
+    constexpr int FE_FX = 0, FE_FU = 8 * NCP, FE_FR = 9 * NCP, FE_SB = 10 * NCP, FE_KU = 10 * NCP + 8 * MCP,
+                  FE_W0 = 10 * NCP + 9 * MCP, FE_E = 10 * NCP + 10 * MCP, FE_D = 10 * NCP + 11 * MCP,
+                  FE_TOT = 11 * NCP + 11 * MCP;
     __shared__ double fe[FE_TOT];
     // (an MPC step: every phase builds q, u from X, U; phase 0 also publishes them or saves X, U)
     const bool fe_on = a.X != nullptr;
     {
-        const int n = a.n, m = a.m;
+        const int n = a.n, m = a.m, nx = fe_on ? a.nx : 0;
+        for (int i = threadIdx.x; i < MCP; i += NTH) fe[FE_E + i] = i < m ? (double)a.ops.E[i] : 0.0;
+        for (int i = threadIdx.x; i < NCP; i += NTH) fe[FE_D + i] = i < n ? (double)a.ops.D[i] : 0.0;
         if (fe_on) {
+            for (int i = threadIdx.x; i < 8 * NCP; i += NTH) {
+                const int v = i >> 3, t = i & 7;
+                fe[FE_FX + i] = (v < n && t < nx) ? a.Fx[(size_t)v * nx + t] : 0.0;
+            }
+            for (int i = threadIdx.x; i < 8 * MCP; i += NTH) {
+                const int v = i >> 3, t = i & 7;
+                fe[FE_SB + i] = (v < m && t < nx) ? a.Sbar[(size_t)v * nx + t] : 0.0;
+            }
             for (int i = threadIdx.x; i < NCP; i += NTH) fe[FE_FU + i] = i < n ? a.Fu[i] : 0.0;
             for (int i = threadIdx.x; i < MCP; i += NTH) {
                 fe[FE_KU + i] = i < m ? a.Ku[i] : 0.0;
@@ -585,10 +595,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             for (int s = 0; s < KN; s++) {
                 const int v = 4 * s + g;  // < NCP: padded rows of fe are zero
                 double s0 = 0.0;
-                const double *fx = a.Fx + (size_t)(v < n ? v : 0) * nx;
 #pragma unroll
                 for (int t = 0; t < 8; t++)
-                    if (t < nx) s0 += (v < n ? fx[t] : 0.0) * Xv[t];
+                    if (t < nx) s0 += fe[FE_FX + 8 * v + t] * Xv[t];
                 const double s1 = fe[FE_FU + v] * Uv;
                 qk[s] = s0 + s1 + fe[FE_FR + v];
                 if (mpc_fe && a.q_out && pub && v < n) a.q_out[(size_t)b * n + v] = qk[s];
@@ -614,10 +623,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             for (int s = 0; s < KM; s++) {
                 const int v = 4 * s + g;
                 double sx = 0.0;
-                const double *sb = a.Sbar + (size_t)(v < m ? v : 0) * nx;
 #pragma unroll
                 for (int t = 0; t < 8; t++)
-                    if (t < nx) sx += (v < m ? sb[t] : 0.0) * Xv[t];
+                    if (t < nx) sx += fe[FE_SB + 8 * v + t] * Xv[t];
                 up[s] = fe[FE_W0 + v] + sx + fe[FE_KU + v] * Uv;
                 if (mpc_fe && a.u_out && pub && v < m) a.u_out[(size_t)b * m + v] = up[s];
             }
@@ -645,7 +653,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
         for (int s = 0; s < NS; s++) {
             const int v = 4 * s + g;
             const int sk = s < KN ? s : 0;
-            const T qn = (s < KN && v < n) ? (T)((qk[sk] * (double)s_D[v]) * c64) : T(0);
+            const T qn = (s < KN && v < n) ? (T)((qk[sk] * fe[FE_D + v]) * c64) : T(0);
             if (fill[gi]) {
                 qh[gi][s] = qn;
                 if (s < KN) s_qh[threadIdx.x >> 6][gi * KN + sk][lane] = qn;
@@ -660,7 +668,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             const int v = 4 * s + g;
             double uu = kInfty, ll = -kInfty;
             if (s < KM && v < m) {
-                const double e = (double)s_E[v];  // osqp_update_bounds: u^ = E u, l^ = E l
+                const double e = fe[FE_E + v];  // osqp_update_bounds: u^ = E u, l^ = E l
                 uu = up[s] * e;
                 if constexpr (!LFREE) ll = lo[s] * e;
                 if (!resume) {  // a resumed phase's QPs passed these checks in phase 0
@@ -688,7 +696,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     MPCQ_PRO_MARK(14);
 
     // g = W' q^ (the q-part of the KKT right-hand side in the W-basis)
-    tile_mv_g<T, G, NT, KN, KNP>(gimg + L.Wt, qh, gv, lane, nullptr);
+    tile_mv_g<T, G, NT, KN, KNP>(img + L.Wt, qh, gv, lane, nullptr);
 #pragma unroll
     for (int gi = 0; gi < G; gi++)
 #pragma unroll
@@ -756,7 +764,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     auto finalize = [&](const bool (&mine)[G], const double *Uold) {
         // x = D W x'  (all lanes run the MFMA; `mine` lanes store)
         T xh[G][NS];
-        tile_mv_g<T, G, NT, KN, KNP>(gimg + L.W, xs, xh, lane, nullptr);
+        tile_mv_g<T, G, NT, KN, KNP>(img + L.W, xs, xh, lane, nullptr);
         const double cinv64 = (double)op.cs[1];
 #pragma unroll
         for (int gi = 0; gi < G; gi++) {
@@ -1613,7 +1621,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             }
             if (!wave_any(anyc)) return;
             T t1[G][NS], ndx[G];
-            tile_mv_g<T, G, NT, KN, KNP>(gimg + L.W, dx, t1, lane, nullptr);
+            tile_mv_g<T, G, NT, KN, KNP>(img + L.W, dx, t1, lane, nullptr);
             const T *D = fresh_ptr((const T *)s_D);
             const T cs = scaled_term ? T(1) : op.cs[0];
             anyc = false;
@@ -1890,7 +1898,7 @@ int tile_launch(const AdmmArgs<T> &a, hipStream_t s)
                 // f32 at 2 waves/SIMD (AdmmArgs::tile_occ): a batch of 2 k rounds of 2,048 wave slots runs
                 // without the lone-wave last round 3 waves/SIMD leave (4,096 waves on 3,072 slots); the
                 // registers allow 3, so dynamic LDS holds a CU to 2 workgroups (> 160 KiB / 3 each)
-                if (a.tile_occ == 2) return tile_launch_variant<T, KN, KM, true, true, 1, OCC, true>(a, s, 28 * 1024);
+                if (a.tile_occ == 2) return tile_launch_variant<T, KN, KM, true, true, 1, OCC, true>(a, s, 16 * 1024);
             }
             return tile_launch_variant<T, KN, KM, true, true, 1, OCC, true>(a, s);
         }

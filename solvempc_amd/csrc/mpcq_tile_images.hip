@@ -20,8 +20,8 @@ __global__ void tile_images_kernel(const double *ops, int nc, int mc, int KN, in
         const bool pset = e0 >= LG.total;
         const TileLayout &L = pset ? LP : LG;
         const size_t e = pset ? e0 - LG.total : e0;
-        // which image (ids in storage order: 0 S, 1 Bt, 2 B, 3 PW, 4 AhT, 5 BS, 6 W, 7 Wt)
-        const size_t offs[8] = {L.S, L.Bt, L.B, L.PW, L.AhT, L.BS, L.W, L.Wt};
+        // which image
+        const size_t offs[8] = {L.S, L.Bt, L.B, L.PW, L.AhT, L.W, L.Wt, L.BS};
         int id = 7;
         while (id > 0 && e < offs[id]) id--;
         const bool out_m = id == 2 && !pset;                // B has m output rows
@@ -37,7 +37,7 @@ __global__ void tile_images_kernel(const double *ops, int nc, int mc, int KN, in
         const int s = sg * VEC + within;
         const int row = 16 * t + tile_arow(is32, lane & 15);
         const int col = 4 * s + (lane >> 4);
-        const int rows = out_m ? mc : (id == 5 ? 8 * KN : (pset && id == 2 ? 4 * KN : nc)), cols = in_m ? mc : nc;
+        const int rows = out_m ? mc : (id == 7 ? 8 * KN : (pset && id == 2 ? 4 * KN : nc)), cols = in_m ? mc : nc;
         double v = 0.0;
         if (row < rows && col < cols && s < (in_m ? KM : KN)) {
             switch (id) {
@@ -46,12 +46,12 @@ __global__ void tile_images_kernel(const double *ops, int nc, int mc, int KN, in
             case 2: v = ops[O.WtA + (size_t)row * nc + col]; break;
             case 3: v = ops[O.PW + (size_t)row * nc + col]; break;
             case 4: v = ops[O.Ah + (size_t)col * nc + row]; break;
-            case 5:  // BS: B~ rows, then S rows from 4 KN on
+            case 5: v = ops[O.W + (size_t)row * nc + col]; break;
+            case 6: v = ops[O.W + (size_t)col * nc + row]; break;
+            default:  // BS: B~ rows, then S rows from 4 KN on
                 if (row < 4 * KN) v = row < nc ? ops[O.WtA + (size_t)row * nc + col] : 0.0;
                 else v = row - 4 * KN < nc ? ops[O.sWtW + (size_t)(row - 4 * KN) * nc + col] : 0.0;
                 break;
-            case 6: v = ops[O.W + (size_t)row * nc + col]; break;
-            default: v = ops[O.W + (size_t)col * nc + row]; break;
             }
         }
         img[e0] = (T)v;
