@@ -77,3 +77,31 @@ def test_condense_from_json_shapes():
         mpc.from_json([[1, 2], [3]], 2, 2)
     with pytest.raises(mpc.JsonTypeError):
         mpc.from_json([1, 2, 3], 4, 1)
+
+
+def test_header_constants_match_the_mirror():
+    """The precision constants of include/mpcq.h (MPCQ_F64 / F32 / F64_MIXED and the mixed path's fp64
+    share MPCQ_MIX_R) are the ctypes mirror's: bench.py prices the mixed FLOP split with the latter."""
+    hdr = (ROOT / "include" / "mpcq.h").read_text()
+    for name in ("MPCQ_F64", "MPCQ_F32", "MPCQ_F64_MIXED", "MPCQ_MIX_R"):
+        m = re.search(rf"#define {name} (\d+)", hdr)
+        assert m and int(m.group(1)) == getattr(_capi, name), name
+
+
+def test_flop_accounting_helpers():
+    """workload's FLOP counts: the mixed split adds up to the total (per solve and over a stream whose solves
+    stop on check iterations), and the fp64 per-plant kernel's one-GEMV count is below the two-product one
+    by exactly the per-iteration and per-factorisation difference."""
+    from solvempc_amd import workload as w
+    it = np.array([25, 50, 75, 100, 125, 225, 13])
+    f64, f32 = w.flops_split_mixed(20, 40, 4, it, 5, paired=True)
+    assert np.allclose(f64 + f32, w.flops_per_qp(20, 40, 4, it, paired=True))
+    assert np.all(f32[:6] == (it[:6] - (it[:6] // 25) * 5) * w._flop_terms(20, 40, 4, True)[0])
+    tot = np.array([25 * 1000, 25 * 1003, 50 * 1000])
+    g64, g32 = w.flops_split_mixed_total(20, 40, 4, tot, 1000, 5, paired=True)
+    assert np.allclose(g64 + g32, w.flops_per_qp_total(20, 40, 4, tot, 1000, paired=True))
+    iters, ref = np.array([97.0, 125.0]), np.array([0.0, 1.0])
+    a = w.flops_plant_step(20, 4, iters, ref)
+    b = w.flops_plant_step(20, 4, iters, ref, merged=True)
+    N = 20
+    assert np.allclose(a - b, iters * (2 * N * N - 5 * N) + (1 + ref) * 4 * N * N)
