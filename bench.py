@@ -397,9 +397,14 @@ def main_dry(a, rank, world, dist):
     _, U = workload.mpc_states(a.seed, start, count)
     U_t = torch.zeros(pad, dtype=torch.float64)
     U_t[:count] = torch.from_numpy(U)
-    gathered = [torch.empty_like(U_t) for _ in range(world)] if rank == 0 else None
-    wall, got = _timed_loop(a, lambda i=None: mdist.gather_moves(dist, U_t, world, rank, gathered), dist, world,
-                            torch.device("cpu"))
+    pg = mdist.PipelinedGather(dist, world, rank, U_t.clone())  # (the bench's overlapped per-step gather)
+
+    def step(i=None):
+        pg.buffer().copy_(U_t)
+        return pg.gather()
+
+    wall, got = _timed_loop(a, step, dist, world, torch.device("cpu"))
+    pg.finish()
     if rank != 0:
         return None
     rec = _header(a, world, None, wall, a.dtype, "QP solves/sec (n_x=4, n_u=1, N=20 batch)",
@@ -488,6 +493,10 @@ def main_lti(a, rank, world, local, dist, dev):
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
     gathered = [torch.empty_like(U_d) for _ in range(world)] if rank == 0 else None
+    # the per-step gather of the moves overlaps the next step (double-buffered U, async RCCL gather); the
+    # stream workload (tens of ms per step) gathers in line
+    pg = mdist.PipelinedGather(dist, world, rank, U_d) if not stream_mode else None
+    U_line = U_d
 
     if stream_mode:
         solver.mpc_set_plant(plant["Ad"], plant["Bd"])
@@ -498,6 +507,7 @@ def main_lti(a, rank, world, local, dist, dev):
     cur = torch.cuda.current_stream(dev)
 
     def step(i=None):
+        U_d = pg.buffer() if pg else U_line
         U_d.copy_(U0_d)          # every step: the reference's first control step of each plant
         if not perplant:         # (perplant: the setup inside the step resets the state)
             solver.reset_state()  # post-setup solver state (x = z = y = 0, rho = settings.rho)
@@ -519,9 +529,12 @@ def main_lti(a, rank, world, local, dist, dev):
             ev[i][1].record(stream)
         if stream_mode:
             cur.wait_stream(stream)
-        return mdist.gather_moves(dist, U_d, world, rank, gathered)
+            return mdist.gather_moves(dist, U_d, world, rank, gathered)
+        return pg.gather()
 
     wall, got = _timed_loop(a, step, dist, world, dev)
+    if pg:
+        U_d = pg.finish()  # the last step's moves
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
     U_out = U_d[:B].cpu().numpy().copy()  # this step's applied U (the parity block's device side)
 

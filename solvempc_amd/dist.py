@@ -36,3 +36,48 @@ def gather_moves(dist, moves, world: int, rank: int, gathered=None):
         gathered = [moves.new_empty(moves.shape) for _ in range(world)]
     dist.gather(moves, gathered if rank == 0 else None, dst=0)
     return gathered if rank == 0 else None
+
+
+class PipelinedGather:
+    """The per-step gather of the applied moves, overlapped with the next step.  Step i writes its moves
+    into one of two buffers that alternate and issues their gather asynchronously (``async_op=True``: on
+    RCCL the collective runs on the communicator's own stream, ordered after the kernels that produced the
+    moves), so step i + 1's solve runs while step i's moves travel over xGMI.  A buffer is written again
+    only after its previous gather has been made a dependency of the current stream (``work.wait()``: no
+    host stall on RCCL).  World size 1: one buffer, nothing to gather."""
+
+    def __init__(self, dist, world: int, rank: int, like):
+        self.dist, self.world, self.rank = dist, world, rank
+        self.bufs = [like] if world == 1 else [like, like.clone()]
+        self.work = [None] * len(self.bufs)
+        self.gathered = ([[like.new_empty(like.shape) for _ in range(world)] for _ in self.bufs]
+                         if rank == 0 and world > 1 else None)
+        self.k = 0
+        self.last = 0
+
+    def buffer(self):
+        """The buffer this step writes its moves into (its previous gather is waited on first)."""
+        if self.work[self.k] is not None:
+            self.work[self.k].wait()
+            self.work[self.k] = None
+        return self.bufs[self.k]
+
+    def gather(self):
+        """Issue this step's gather (rank 0 receives into its per-buffer list); returns that list on rank
+        0, None elsewhere (world 1: [moves])."""
+        k = self.k
+        self.last = k
+        self.k = (k + 1) % len(self.bufs)
+        if self.world == 1:
+            return [self.bufs[k]]
+        self.work[k] = self.dist.gather(self.bufs[k], self.gathered[k] if self.rank == 0 else None, dst=0,
+                                        async_op=True)
+        return self.gathered[k] if self.rank == 0 else None
+
+    def finish(self):
+        """Wait for every outstanding gather; returns the last step's moves (this rank's buffer)."""
+        for i, w in enumerate(self.work):
+            if w is not None:
+                w.wait()
+                self.work[i] = None
+        return self.bufs[self.last]
