@@ -671,6 +671,7 @@ template <typename T, int NC>
 int plant_step_launch_t(const PlantStepArgs &a, hipStream_t s)
 {
     if (NC <= 20 && a.wpe == 3) hipLaunchKernelGGL((plant_step_kernel<T, NC, 3>), dim3((a.n_plants + 1) / 2), dim3(64), 0, s, a);
+    else if (NC <= 20 && a.wpe == 4) hipLaunchKernelGGL((plant_step_kernel<T, NC, 4>), dim3((a.n_plants + 1) / 2), dim3(64), 0, s, a);
     else hipLaunchKernelGGL((plant_step_kernel<T, NC, 2>), dim3((a.n_plants + 1) / 2), dim3(64), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
