@@ -50,7 +50,7 @@ constexpr int kMaxPhases = 16;
 //   MPCQ_TAIL=wave|tile         the tile chain's last launch on the one-QP-per-wave / tile kernel
 //   MPCQ_MIX_R=r                MPCQ_F64_MIXED: fp64 iterations per check interval (default MPCQ_MIX_R)
 //   MPCQ_TILE_OCC=2|3           waves per SIMD of the f32 paired tile kernel (default 3)
-//   MPCQ_PLANT_WPE=2|3          waves per SIMD of the one-pass per-plant kernel (default f64 3, f32 2)
+//   MPCQ_PLANT_WPE=2|3|4        waves per SIMD of the one-pass per-plant kernel (default f64 3, f32 2)
 // Debug builds (-DMPCQ_DEBUG_HOOKS) add the stamp / profiling dumps (MPCQ_TILE_STAMPS,
 // MPCQ_SETUP_PROF, MPCQ_MIMO_SETUP_STAMPS, MPCQ_MIMO_STAMPS) and MPCQ_DEBUG_SYNC.
 const char *test_hook(const char *name)
