@@ -1283,8 +1283,10 @@ static int launch_tile_stream(mpcq_ctx *c, hipStream_t s, double *X, double *U, 
     if (ct <= 0 || st.max_iter % ct || (st.adaptive_rho && a.adaptive_interval % ct)) return -1;
     const char *e = test_hook("MPCQ_STREAM_CPW");
     const long simds = (long)c->cus * 4;
-    sa.cpw = *e ? std::max(1, std::min(16, std::atoi(e)))
-                : (int)std::max<long>(1, std::min<long>(16, ((long)c->dims.batch + simds - 1) / simds));
+    // plants per wave: one wave per SIMD (f32, 4 at 4,096 plants), twice that for fp64 / mixed, whose waves
+    // measured faster at half the SIMDs (config 5: cpw 4 103.7 M QP/s, 6-16 105.5-106.3 M, r04w_*)
+    const long per = ((long)c->dims.batch + simds - 1) / simds * (c->dims.dtype == MPCQ_F32 ? 1 : 2);
+    sa.cpw = *e ? std::max(1, std::min(16, std::atoi(e))) : (int)std::max<long>(1, std::min<long>(16, per));
     a.mpc = 1; a.mpc_u = 1; a.nx = c->nx; a.X = X; a.U = U; a.xref = xref;
     a.Fx = c->d_Fx; a.Fu = c->d_Fu; a.Fr = c->d_Fr; a.Sbar = c->d_Sbar; a.Ku = c->d_Ku; a.W0 = c->d_W0;
     a.X_save = c->d_Xs; a.U_save = c->d_Us;  // the last step's X, U: its q, u on demand (materialize_qu)
