@@ -49,9 +49,36 @@ template <typename T, typename F> __device__ __forceinline__ T half_reduce(T v, 
     v = op(v, dpp_t<0x140>(v));  // row_mirror
     return swap16(v, op);
 }
+// max / max of magnitudes as single v_max instructions (|.| as a source modifier).  LLVM's maxnum adds a
+// canonicalising v_max x, x per operand here; on the finite, non-NaN values these norms and scalings see
+// the results are the same (max is exact).
+__device__ __forceinline__ double hwmax(double a, double b)
+{
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float hwmax(float a, float b)
+{
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double hwmax_abs(double m, double x)  // max(m, |x|)
+{
+    double r;
+    asm("v_max_f64 %0, %1, |%2|" : "=v"(r) : "v"(m), "v"(x));
+    return r;
+}
+__device__ __forceinline__ double hwmax_abs2(double x, double y)  // max(|x|, |y|)
+{
+    double r;
+    asm("v_max_f64 %0, |%1|, |%2|" : "=v"(r) : "v"(x), "v"(y));
+    return r;
+}
 template <typename T> __device__ __forceinline__ T hmax(T v)
 {
-    return half_reduce(v, [](T a, T b) { return tt_fmax(a, b); });
+    return half_reduce(v, [](T a, T b) { return hwmax(a, b); });
 }
 template <typename T> __device__ __forceinline__ T hsum(T v)
 {
@@ -303,11 +330,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     const double aK0 = fabs(K0);
     double Dr = lr ? 1.0 : 0.0, Er = lr ? 1.0 : 0.0;  // (0 on dead lanes: neutral in every scan)
     double cost = 1.0, cp = 1.0;
-    auto dmax = [](double x, double y) { return fmax(x, y); };
+    auto dmax = [](double x, double y) { return hwmax(x, y); };
     for (int it = 0; it < st.scaling; it++) {
         double vp = 0.0;
 #pragma unroll
-        for (int j = 0; j < NC; j++) vp = fmax(vp, fabs(pr[j]));
+        for (int j = 0; j < NC; j++) vp = hwmax_abs(vp, pr[j]);
         const double emax = half_suffix(Er, dmax, lane), dpre = half_prefix(Dr, dmax);
         const double va = (aK0 * Dr) * emax, ve = (aK0 * Er) * dpre;
         const double dt = 1.0 / sqrt(limit_scaling_p(fmax(cp * vp, va)));
@@ -320,7 +347,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
             const double2 d2 = *(const double2 *)(S.tmp + j);
             pr[j] = (dt * (pr[j] * cp)) * d2.x;
             pr[j + 1] = (dt * (pr[j + 1] * cp)) * d2.y;
-            cn = fmax(cn, fmax(fabs(pr[j]), fabs(pr[j + 1])));
+            cn = hwmax(cn, hwmax_abs2(pr[j], pr[j + 1]));
         }
         wave_sync();
         if (lr) { Dr *= dt; Er *= et; }
@@ -559,10 +586,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         TD dr_r = 0, dr_s = 0, qn_r = 0, qn_s = 0, atyn_r = 0, atyn_s = 0, pxn_r = 0, pxn_s = 0;
         if (lr) {
             const TD r1 = ax - ztd, r2 = -ax - zbd;
-            ax_z = fmax(fabs(r1), fabs(r2));
-            ax_zs = fmax(fabs(EiD * r1), fabs(EiD * r2));
-            zn_r = fmax(fabs(ztd), fabs(zbd));
-            zn_s = fmax(fabs(EiD * ztd), fabs(EiD * zbd));
+            ax_z = hwmax_abs2(r1, r2);
+            ax_zs = hwmax_abs2(EiD * r1, EiD * r2);
+            zn_r = hwmax_abs2(ztd, zbd);
+            zn_s = hwmax_abs2(EiD * ztd, EiD * zbd);
             axn_r = fabs(ax);
             axn_s = fabs(EiD * ax);
             const TD rd = (qsl + px) + aty;
