@@ -111,3 +111,30 @@ def test_bench_strong_scaling_splits_one_global_batch():
     assert rec["config"]["batch_per_gpu"] == 501  # rank 0's block
     assert rec["collective"]["gathered"] == 1001 and rec["collective"]["matches_stream"] is True
     assert 1 << 20 == __import__("bench").parse(["--workload", "perplant", "--scaling", "strong"]).global_batch
+
+
+def test_bench_under_torch_distributed_run():
+    """The driver's launcher: `python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr
+    127.0.0.1 --master-port P bench.py --gpus 2 ...` (the ranks come from the launcher, bench.py spawns
+    none); four steps of the overlapped per-step gather over gloo reach rank 0 intact."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), str(root / "bench.py"),
+                        "--gpus", "2", "--backend", "gloo", "--dry-run", "--steps", "4", "--warmup", "2",
+                        "--batch", "777"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["steps"] == 4 and rec["warmup"] == 2
+    assert rec["collective"] == {"backend": "gloo", "world_size": 2, "gathered": 1554, "matches_stream": True}
