@@ -316,6 +316,16 @@ def test_full_batch_mpc_step_matches_oracle(plant, tail, monkeypatch):
     assert np.abs((Ug - U) - np.where(st == sm.SOLVED, x[:, 0], 0.0)).max() <= 1e-12 * max(1.0, np.abs(Ug).max())
     if off.any():
         _osqp_terminated(x[off], s.dual()[off], q[off], u[off], ops)
+    if tail == "wave":  # the variant ran its tail: QPs past 125 iterations exist (one QP per wave there)
+        assert (it > 5 * 25).any()
+    # the step's q, u as the solver keeps them (materialised from the saved X, U, after the tail's own
+    # front end rebuilt them for its QPs) are the oracle's updateGradient / updateUpperBound data
+    v = s.device_view()
+    torch.cuda.synchronize()
+    qd = torch.as_tensor(_DevArray(v["q"], (B, N)), device="cuda").cpu().numpy()
+    ud = torch.as_tensor(_DevArray(v["u"], (B, 2 * N)), device="cuda").cpu().numpy()
+    assert np.abs(qd - q).max() <= 1e-12 * max(1.0, np.abs(q).max())
+    assert np.abs(ud - u).max() <= 1e-12 * max(1.0, np.abs(u).max())
     print(f"fp32 bench path: {int(off.sum())} of {B} QPs took a tie's other branch")
 
 
