@@ -11,5 +11,10 @@ for rep in 1 2 3; do
     MPCQ_PLANT_WPE=$w timeout -k 10 200 python bench.py --workload perplant --steps 5 --warmup 2 --cpu-seconds 0 > gpurun_out/w_wpe${w}_$rep.json 2>> gpurun_out/w.err || exit $?
   done
 done
+for rep in 1 2; do
+  for cpw in 6 8 12 16; do
+    MPCQ_STREAM_CPW=$cpw timeout -k 10 200 python bench.py --workload stream --dtype f64 --steps 2 --warmup 1 --cpu-seconds 0 > gpurun_out/w_st_cpw${cpw}_$rep.json 2>> gpurun_out/w.err || exit $?
+  done
+done
 DT=f64 bash tools/prof_cfg3.sh || exit $?
 exit 0
