@@ -53,6 +53,9 @@ def _run_device(shared, Ad, Bd, X, U, N, s_rows=None, yref=None, steps=1, settin
     return Us, s.solution(), st, it
 
 
+TIE_X_REL = 5e-2  # a tie's solution against the oracle's (as for config 3's fp32 ties, test_plants_step.py)
+
+
 def _check(x, st, it, U1, x_ref, st_ref, it_ref, U_ref, margin, tol=1e-7):
     assert np.array_equal(st, st_ref), (st, st_ref)
     same = it == it_ref
@@ -62,6 +65,9 @@ def _check(x, st, it, U1, x_ref, st_ref, it_ref, U_ref, margin, tol=1e-7):
     rel = np.abs(x[same] - x_ref[same]).max(axis=1) / np.maximum(1.0, np.abs(x_ref[same]).max(axis=1))
     assert rel.max() < tol, rel.max()
     assert np.abs(U1[same] - U_ref[same]).max() < tol
+    if not same.all():  # a tie stops one check earlier or later: both iterates met eps 1e-3, so they agree loosely
+        rt = np.abs(x[~same] - x_ref[~same]).max(axis=1) / np.maximum(1.0, np.abs(x_ref[~same]).max(axis=1))
+        assert rt.max() < TIE_X_REL, rt.max()
 
 
 def test_quadrotor_step_matches_oracle():
