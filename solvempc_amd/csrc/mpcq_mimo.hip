@@ -546,12 +546,28 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
     const bool valid = c < NU && k < N;
     const int e = valid ? k * NU + c : 0;  // natural index (masked when !valid)
     const int vi = c * 32 + (k & 31);      // component-major slot
+    // ONE (n_u = 4, diagonal K0): the matrix rows are permuted so that wave c holds the rows of
+    // component c, row group rg = 8 c + j register i = (block 4 j + i, component c): the GEMV output a
+    // lane consumes is produced inside its own wave (a lane permute, no LDS round trip, no barrier),
+    // and an iteration has one barrier (the rhs, double-buffered).  Otherwise row group rg holds the
+    // natural rows 4 rg .. 4 rg + 3.
+    constexpr bool ONE = NU == 4 && DK;
+    // (r = rg laundered through an empty asm at the use: hoisted out of the solve loop, these
+    // indices would hold registers the matrix needs)
+    auto row_nat = [](int r, int i) { return ONE ? 16 * (r & 7) + 4 * i + (r >> 3) : 4 * r + i; };
+    auto row_blk = [](int r, int i) { return ONE ? 4 * (r & 7) + i : (4 * r) / NU + i / NU; };
+    auto row_cmp = [](int r, int i) { return ONE ? r >> 3 : i % NU; };
+    auto rg_here = [&]() {
+        int r = rg;
+        if (ONE) asm volatile("" : "+v"(r));
+        return r;
+    };
     MPCQ_MSTAMP(0, __builtin_amdgcn_s_memtime());
 
     // GEMV inputs and the Gauss-Jordan row broadcast: natural order in 16-element segments padded to
     // 18 (kSegLd), so the 8 column groups' 16-B reads fall in distinct LDS banks; the GEMV output is
     // component-major (the vector role reads it lane-consecutively)
-    __shared__ __attribute__((aligned(16))) double s_vec[kSegN];   // rhs (GEMV input)
+    __shared__ __attribute__((aligned(16))) double s_vec[2][kSegN];  // rhs (GEMV input; alternating in ONE)
     __shared__ __attribute__((aligned(16))) double s_nat[kSegN];   // warm start: x
     __shared__ __attribute__((aligned(16))) double s_out[kMimoN];  // GEMV output, component-major
     __shared__ __attribute__((aligned(16))) double s_row[2][kSegN];
@@ -564,7 +580,7 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
         s_D[i] = ok ? ops[L.D + kk * NU + cc] : 1.0;
         s_E[i] = ok ? ops[L.E + kk * NU + cc] : 1.0;
     }
-    for (int i = t; i < kSegN; i += kMimoThreads) s_vec[i] = s_nat[i] = 0.0;
+    for (int i = t; i < kSegN; i += kMimoThreads) s_vec[0][i] = s_vec[1][i] = s_nat[i] = 0.0;
     for (int i = t; i < 16; i += kMimoThreads) {
         const int r = i >> 2, cc = i & 3;
         s_K0[i] = (r < NU && cc < NU) ? ops[L.K0 + r * NU + cc] : 0.0;
@@ -716,9 +732,12 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
         }
         rb ^= 1;
     };
+    int svr = 0, svw = 0;  // the rhs buffer the next GEMV reads / the next rhs goes to
     auto st_rhs = [&](double r) {
         vrhs = r;
-        if (valid) s_vec[seg_of(e)] = r;
+        if (valid) s_vec[svw][seg_of(e)] = r;
+        svr = svw;
+        if (ONE) svw ^= 1;
     };
     auto make_rhs = [&]() {  // rhs = sigma x - q^ + A^'(rho z - y)
         const double d = (rho * vzt - vyt) - (rho * vzb - vyb);
@@ -766,13 +785,14 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
 
     int fail = 0;
     double Mb[4][16];
-    // rows 4 rg + i, columns 16 cg + j (P^ rows are padded to L.ldp: aligned, in-bounds loads);
+    // rows row_nat(i), columns 16 cg + j (P^ rows are padded to L.ldp: aligned, in-bounds loads);
     // the padding beyond n is the identity
     auto load_P = [&]() {
         const int seg = 16 * cg < L.ldp - 16 ? 16 * cg : L.ldp - 16;
+        const int r = rg_here();
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            const int gi = 4 * rg + i;
+            const int gi = row_nat(r, i);
             const double2 *row = (const double2 *)(ops + L.Ph + (size_t)(gi < n ? gi : n - 1) * L.ldp + seg);
 #pragma unroll
             for (int j = 0; j < 8; j++) {
@@ -785,13 +805,14 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
             for (int j = 0; j < 16; j++) asm volatile("" : "+v"(Mb[i][j]));  // one row of loads in flight
         }
     };
-    // + sigma I + r D SW[max(bi, bj)] D on the n x n part (block of row gi: (4 rg + i) / NU)
+    // + sigma I + r D SW[max(bi, bj)] D on the n x n part (block of row gi: row_blk(i))
     auto add_kkt = [&](double r) {
         double di[4];
+        const int rl = rg_here();
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            const int bi = (4 * rg) / NU + i / NU;
-            di[i] = s_D[(i % NU) * 32 + (bi < 31 ? bi : 31)];
+            const int bi = row_blk(rl, i);
+            di[i] = s_D[row_cmp(rl, i) * 32 + (bi < 31 ? bi : 31)];
         }
 #pragma unroll
         for (int jc = 0; jc < 4; jc++) {
@@ -802,7 +823,7 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
                 const double dj = s_D[cj * 32 + (bj < 31 ? bj : 31)];
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-                    const int gi = 4 * rg + i, bi = (4 * rg) / NU + i / NU, ci = i % NU;
+                    const int gi = row_nat(rl, i), bi = row_blk(rl, i), ci = row_cmp(rl, i);
                     const int bm = bi > bj ? bi : bj;
                     const double g = (di[i] * dj) * s_SW[(bm < 31 ? bm : 31) * 16 + ci * 4 + cj];
                     const double v = Mb[i][j] + (gi == gj ? sigma : 0.0) + r * g;
@@ -815,8 +836,8 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
                 for (int jj = 0; jj < 4; jj++) asm volatile("" : "+v"(Mb[i][4 * jc + jj]));  // (as in invert)
         }
     };
-    // outv[4 rg + i] = row (4 rg + i) of M . in (the 8 lanes of a row group combine by DPP)
-    auto gemv = [&](const double *in, double *outv) {
+    // part[i] = row row_nat(i) of M . in, in all 8 lanes of the row group (combined by DPP)
+    auto gemv_rows = [&](const double *in, double (&part)[4]) {
         double s0[4], s1[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) s0[i] = s1[i] = 0.0;
@@ -839,7 +860,6 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
 #pragma unroll
             for (int i = 0; i < 4; i++) asm volatile("" : "+v"(s0[i]), "+v"(s1[i]));  // one chunk live at a time
         }
-        double part[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             part[i] = s0[i] + s1[i];
@@ -847,16 +867,29 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
             part[i] += dpp_t<0x4E>(part[i]);   // quad_perm [2,3,0,1]
             part[i] += dpp_t<0x141>(part[i]);  // row_half_mirror: the other quad of the 8
         }
-        if (cg == 0)  // rows 4 rg + i -> component-major (block (4 rg + i) / NU, component (4 rg + i) % NU)
+    };
+    // outv[component-major slot of row_nat(i)] = row row_nat(i) of M . in
+    auto gemv = [&](const double *in, double *outv) {
+        double part[4];
+        gemv_rows(in, part);
+        if (cg == 0)
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const int bk = (4 * rg) / NU + i / NU;
-                if (4 * rg + i < n) outv[(i % NU) * 32 + bk] = part[i];
-            }
+            for (int i = 0; i < 4; i++)
+                if (row_nat(rg, i) < n) outv[row_cmp(rg, i) * 32 + row_blk(rg, i)] = part[i];
+    };
+    // ONE: this lane's element (block k, component c) of M . in, from lane 8 (k >> 2) + (k & 3) of the
+    // same wave, whose register row (its cg & 3) is block k
+    auto gemv_own = [&](const double *in) {
+        double part[4];
+        gemv_rows(in, part);
+        const int ci = cg & 3;
+        const double sel = ci == 0 ? part[0] : ci == 1 ? part[1] : ci == 2 ? part[2] : part[3];
+        return __shfl(sel, 8 * ((k >> 2) & 7) + (k & 3), 64);
     };
     // Gauss-Jordan: a_ij -= (a_ik / a_kk) a_kj everywhere, then row k <- a_kj / a_kk, column k <-
     // -a_ik / a_kk, a_kk <- 1 / a_kk.  k = 16 kb + kk with kk unrolled: the owner of column k is
-    // cg == kb (register column kk), of row k rg == k >> 2 (register row kk & 3).  The critical path
+    // cg == kb (register column kk), of row k rg == k >> 2 (register row kk & 3; ONE: rg == 8 (kk & 3)
+    // + kb, register row kk >> 2).  The critical path
     // of a step is barrier -> LDS reads -> 64 FMAs -> next writes: the next pivot's reciprocal is
     // computed one step ahead (its element is updated first, the division overlaps the FMAs) and
     // broadcast with the row, and the row owners scale their row in registers before the update.
@@ -869,12 +902,13 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
                 const int kp = 16 * kb + kk;
                 if (kp >= n) continue;  // (not break: the loop must fully unroll, or Mb leaves the VGPRs)
                 const int p = kp & 1;
-                const bool rown = rg == (kp >> 2), coln = cg == kb;
+                const int rr = ONE ? kk >> 2 : kk & 3, nr = ONE ? ((kk + 1) >> 2) & 3 : (kk + 1) & 3;
+                const bool rown = ONE ? rg == 8 * (kk & 3) + kb : rg == (kp >> 2), coln = cg == kb;
                 if (rown) {  // row k, and (a_kk, 1 / a_kk) in the padding of the pivot's segment
                     double2 *r2 = (double2 *)&s_row[p][kSegLd * cg];
 #pragma unroll
-                    for (int j = 0; j < 8; j++) r2[j] = make_double2(Mb[kk & 3][2 * j], Mb[kk & 3][2 * j + 1]);
-                    if (coln) r2[8] = make_double2(Mb[kk & 3][kk], inv_next);
+                    for (int j = 0; j < 8; j++) r2[j] = make_double2(Mb[rr][2 * j], Mb[rr][2 * j + 1]);
+                    if (coln) r2[8] = make_double2(Mb[rr][kk], inv_next);
                 }
                 __syncthreads();
 #ifdef MPCQ_GJ_STAMPS
@@ -889,7 +923,12 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
                 // column k from row k: the trailing block stays symmetric (a_ik = a_ki, i >= k) and the
                 // pivoted rows are its negation (a_ik = -a_ki, i < k: [A11^-1, A11^-1 A12; -A21 A11^-1, S])
                 double nci[4];  // -a_ik / a_kk (0 on row k itself: its owners scale it instead)
-                {
+                if constexpr (ONE) {  // columns 16 (rg & 7) + 4 i + (rg >> 3)
+                    const int r = rg_here();
+                    const double *c1 = &s_row[p][kSegLd * (r & 7) + (r >> 3)];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) nci[i] = (row_nat(r, i) < kp ? c1[4 * i] : -c1[4 * i]) * inv;
+                } else {
                     const double2 *c2 = (const double2 *)&s_row[p][kSegLd * (rg >> 2) + 4 * (rg & 3)];
                     const double2 u0 = c2[0], u1 = c2[1];
                     const double cv[4] = {u0.x, u0.y, u1.x, u1.y};
@@ -898,7 +937,7 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
                 }
                 // lookahead: the next pivot's element first, its reciprocal overlapping the FMAs
                 {
-                    const int ni = (kk + 1) & 3, nj = (kk + 1) & 15;
+                    const int ni = nr, nj = (kk + 1) & 15;
                     const double rn = s_row[p][seg_of(kp + 1 < kMimoN ? kp + 1 : kp)];
 #ifdef MPCQ_GJ_NODIV
                     inv_next = __builtin_fma(nci[ni], rn, Mb[ni][nj]);
@@ -907,9 +946,9 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
 #endif
                 }
                 if (rown) {
-                    nci[kk & 3] = 0.0;
+                    nci[rr] = 0.0;
 #pragma unroll
-                    for (int j = 0; j < 16; j++) Mb[kk & 3][j] *= inv;  // row k <- a_kj / a_kk
+                    for (int j = 0; j < 16; j++) Mb[rr][j] *= inv;  // row k <- a_kj / a_kk
                 }
 #pragma unroll
                 for (int h = 0; h < 4; h++) {  // 4-column chunks (register budget), the next one in flight
@@ -939,7 +978,7 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
                 if (coln) {
 #pragma unroll
                     for (int i = 0; i < 4; i++) Mb[i][kk] = nci[i];
-                    if (rown) Mb[kk & 3][kk] = inv;
+                    if (rown) Mb[rr][kk] = inv;
                 }
 #ifdef MPCQ_GJ_STAMPS
                 if (a.stamps && kp == 40 && (t == 0 || t == 80)) {
@@ -980,8 +1019,15 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
             }
             refactor = false;
         }
-        gemv(s_vec, s_out);
-        __syncthreads();  // x~ ready
+        double xt;
+        if constexpr (ONE) {
+            xt = gemv_own(s_vec[svr]);
+        } else {
+            gemv(s_vec[svr], s_out);
+            __syncthreads();  // x~ ready
+            xt = s_out[vi];
+        }
+        xt = valid ? xt : 0.0;
         it++;
         const bool at_check = it == next_check, at_adapt = it == next_adapt;
         if (at_check) next_check += ct;
@@ -990,7 +1036,6 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
         const bool info = at_check || at_adapt || last;
         const double rinv = 1.0 / rho;
         // ---- x~ = M^-1 rhs ; z~ = A^ x~ ; P^ x~ = rhs - sigma x~ - rho A^'z~ ; relax ; project ; dual
-        const double xt = valid ? s_out[vi] : 0.0;
         const double ztl = A_of(xt);
         double d2, dr, xn;
         {
