@@ -41,10 +41,10 @@ __device__ inline double mimo_limit_scaling(double d)
 // inclusive max scans over lanes 0..31 of non-negative values (DPP row shifts read 0 outside the row,
 // then one cross-row readlane); lanes >= 32 are ignored by the callers
 template <int CTRL> __device__ __forceinline__ double dpp_zero(double v)
-{
+{  // (bound_ctrl: a lane without a source reads 0, with no zeroed destination to copy first)
     const unsigned long long u = (unsigned long long)__double_as_longlong(v);
-    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xF, 0xF, false);
-    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, false);
+    const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)u, CTRL, 0xF, 0xF, true);
+    const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, true);
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 __device__ __forceinline__ double readlane_f64(double v, int l)
@@ -486,10 +486,10 @@ __device__ __forceinline__ void stb(double *arr, int lane, const B4 &x)
 }
 // DPP move whose lanes without a source read 0 (row shifts)
 template <int CTRL> __device__ __forceinline__ double dpp0(double v)
-{
+{  // (bound_ctrl: a lane without a source reads 0, with no zeroed destination to copy first)
     const unsigned long long u = (unsigned long long)__double_as_longlong(v);
-    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xF, 0xF, false);
-    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, false);
+    const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)u, CTRL, 0xF, 0xF, true);
+    const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, true);
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 __device__ __forceinline__ double readlane_d(double v, int l)
@@ -570,7 +570,7 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
     __shared__ __attribute__((aligned(16))) double s_vec[2][kSegN];  // rhs (GEMV input; alternating in ONE)
     __shared__ __attribute__((aligned(16))) double s_nat[kSegN];   // warm start: x
     __shared__ __attribute__((aligned(16))) double s_out[kMimoN];  // GEMV output, component-major
-    __shared__ __attribute__((aligned(16))) double s_row[2][kSegN];
+    __shared__ __attribute__((aligned(16))) double s_row[2][2][kSegN];  // pivot rows k, k + 1 (alternating)
     __shared__ double s_D[kMimoN], s_E[kMimoN], s_K0[16], s_SW[32 * 16];  // D, E component-major
     __shared__ double s_xb[4][kMimoN];  // scan exchange buffers (rotated: a buffer is rewritten 4 barriers later)
     __shared__ double s_red[2][4][16];  // cross-wave reductions (alternating)
@@ -886,109 +886,120 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
         const double sel = ci == 0 ? part[0] : ci == 1 ? part[1] : ci == 2 ? part[2] : part[3];
         return __shfl(sel, 8 * ((k >> 2) & 7) + (k & 3), 64);
     };
-    // Gauss-Jordan: a_ij -= (a_ik / a_kk) a_kj everywhere, then row k <- a_kj / a_kk, column k <-
-    // -a_ik / a_kk, a_kk <- 1 / a_kk.  k = 16 kb + kk with kk unrolled: the owner of column k is
-    // cg == kb (register column kk), of row k rg == k >> 2 (register row kk & 3; ONE: rg == 8 (kk & 3)
-    // + kb, register row kk >> 2).  The critical path
-    // of a step is barrier -> LDS reads -> 64 FMAs -> next writes: the next pivot's reciprocal is
-    // computed one step ahead (its element is updated first, the division overlaps the FMAs) and
-    // broadcast with the row, and the row owners scale their row in registers before the update.
+    // Gauss-Jordan on pivot pairs K = {k, k + 1} (SPD: no pivoting; n odd pairs the last pivot with
+    // the identity padding, which the update leaves as it is): A <- A - A(:,K) A_KK^-1 A(K,:) off K,
+    // then rows K <- A_KK^-1 A(K,:), columns K <- -A(:,K) A_KK^-1, A_KK <- A_KK^-1.  One LDS broadcast of
+    // the two rows and one barrier per pair; column K is read off the rows (the trailing block stays
+    // symmetric, a_ik = a_ki, and the pivoted rows are its negation, a_ik = -a_ki: [A11^-1,
+    // A11^-1 A12; -A21 A11^-1, S]).  k = 16 kb + kk with kk unrolled: the owner of column k is cg == kb
+    // (register column kk), of row k rg == k >> 2 (register row kk & 3; ONE: rg == 8 (kk & 3) + kb,
+    // register row kk >> 2).  Every thread forms A_KK^-1 from the broadcast (one division); the row
+    // owners' rows restart from 0 and take the same FMA update with multipliers A_KK^-1.
     auto invert = [&]() {
         const int nkb = (n + 15) >> 4;
-        double inv_next = 1.0 / Mb[0][0];  // meaningful on the owner of the next pivot only
         for (int kb = 0; kb < nkb; kb++) {
 #pragma unroll
-            for (int kk = 0; kk < 16; kk++) {
+            for (int kk = 0; kk < 16; kk += 2) {
                 const int kp = 16 * kb + kk;
                 if (kp >= n) continue;  // (not break: the loop must fully unroll, or Mb leaves the VGPRs)
-                const int p = kp & 1;
-                const int rr = ONE ? kk >> 2 : kk & 3, nr = ONE ? ((kk + 1) >> 2) & 3 : (kk + 1) & 3;
-                const bool rown = ONE ? rg == 8 * (kk & 3) + kb : rg == (kp >> 2), coln = cg == kb;
-                if (rown) {  // row k, and (a_kk, 1 / a_kk) in the padding of the pivot's segment
-                    double2 *r2 = (double2 *)&s_row[p][kSegLd * cg];
+                const int p = (kk >> 1) & 1;
+                const int rk = ONE ? kk >> 2 : kk & 3, rl = ONE ? kk >> 2 : (kk & 3) + 1;
+                const bool ownk = ONE ? rg == 8 * (kk & 3) + kb : rg == (kp >> 2);
+                const bool ownl = ONE ? rg == 8 * (kk & 3) + 8 + kb : rg == (kp >> 2);
+                const bool coln = cg == kb;
+                if (ownk) {
+                    double2 *r2 = (double2 *)&s_row[p][0][kSegLd * cg];
 #pragma unroll
-                    for (int j = 0; j < 8; j++) r2[j] = make_double2(Mb[rr][2 * j], Mb[rr][2 * j + 1]);
-                    if (coln) r2[8] = make_double2(Mb[rr][kk], inv_next);
+                    for (int j = 0; j < 8; j++) r2[j] = make_double2(Mb[rk][2 * j], Mb[rk][2 * j + 1]);
+                }
+                if (ownl) {
+                    double2 *r2 = (double2 *)&s_row[p][1][kSegLd * cg];
+#pragma unroll
+                    for (int j = 0; j < 8; j++) r2[j] = make_double2(Mb[rl][2 * j], Mb[rl][2 * j + 1]);
                 }
                 __syncthreads();
-#ifdef MPCQ_GJ_STAMPS
-                if (a.stamps && kp == 40 && (t == 0 || t == 80)) a.stamps[(size_t)blockIdx.x * 8 + (t ? 5 : 2)] = __builtin_amdgcn_s_memtime();
-                if (a.stamps && kp == 41 && t == 0) a.stamps[(size_t)blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memtime();
-#endif
-                const double2 *r2 = (const double2 *)&s_row[p][kSegLd * cg];
-                double2 q0 = r2[0], q1 = r2[1];  // row chunk 0, in flight with the column
-                const double2 pv = *(const double2 *)&s_row[p][kSegLd * kb + 16];
-                if (!(pv.x > 0.0)) fail = 1;
-                const double inv = pv.y;
-                // column k from row k: the trailing block stays symmetric (a_ik = a_ki, i >= k) and the
-                // pivoted rows are its negation (a_ik = -a_ki, i < k: [A11^-1, A11^-1 A12; -A21 A11^-1, S])
-                double nci[4];  // -a_ik / a_kk (0 on row k itself: its owners scale it instead)
+                const double *R0 = s_row[p][0], *R1 = s_row[p][1];
+                const double2 *k2 = (const double2 *)&R0[kSegLd * cg], *l2 = (const double2 *)&R1[kSegLd * cg];
+                double2 qk = k2[0], ql = l2[0];  // row chunk 0, in flight with the pivot block
+                const double2 pk = *(const double2 *)&R0[kSegLd * kb + kk];  // a_kk, a_kl
+                const double all = R1[kSegLd * kb + kk + 1];
+                const double det = __builtin_fma(pk.x, all, -(pk.y * pk.y));
+                if (!(pk.x > 0.0) || !(det > 0.0)) fail = 1;
+                const double idet = 1.0 / det;
+                const double ikk = all * idet, ikl = -pk.y * idet, ill = pk.x * idet;
+                double ck[4], cl[4];  // a_ik, a_il of this thread's rows, read off rows k, l
                 if constexpr (ONE) {  // columns 16 (rg & 7) + 4 i + (rg >> 3)
                     const int r = rg_here();
-                    const double *c1 = &s_row[p][kSegLd * (r & 7) + (r >> 3)];
+                    const int o = kSegLd * (r & 7) + (r >> 3);
 #pragma unroll
-                    for (int i = 0; i < 4; i++) nci[i] = (row_nat(r, i) < kp ? c1[4 * i] : -c1[4 * i]) * inv;
-                } else {
-                    const double2 *c2 = (const double2 *)&s_row[p][kSegLd * (rg >> 2) + 4 * (rg & 3)];
-                    const double2 u0 = c2[0], u1 = c2[1];
-                    const double cv[4] = {u0.x, u0.y, u1.x, u1.y};
-#pragma unroll
-                    for (int i = 0; i < 4; i++) nci[i] = (4 * rg + i < kp ? cv[i] : -cv[i]) * inv;
-                }
-                // lookahead: the next pivot's element first, its reciprocal overlapping the FMAs
-                {
-                    const int ni = nr, nj = (kk + 1) & 15;
-                    const double rn = s_row[p][seg_of(kp + 1 < kMimoN ? kp + 1 : kp)];
-#ifdef MPCQ_GJ_NODIV
-                    inv_next = __builtin_fma(nci[ni], rn, Mb[ni][nj]);
-#else
-                    inv_next = 1.0 / __builtin_fma(nci[ni], rn, Mb[ni][nj]);
-#endif
-                }
-                if (rown) {
-                    nci[rr] = 0.0;
-#pragma unroll
-                    for (int j = 0; j < 16; j++) Mb[rr][j] *= inv;  // row k <- a_kj / a_kk
-                }
-#pragma unroll
-                for (int h = 0; h < 4; h++) {  // 4-column chunks (register budget), the next one in flight
-                    double2 n0 = q0, n1 = q1;
-                    if (h < 3) {
-                        n0 = r2[2 * h + 2];
-                        n1 = r2[2 * h + 3];
+                    for (int i = 0; i < 4; i++) {
+                        ck[i] = R0[o + 4 * i];
+                        cl[i] = R1[o + 4 * i];
                     }
-                    const double rj[4] = {q0.x, q0.y, q1.x, q1.y};
-#ifndef MPCQ_GJ_NOFMA
+                } else {
+                    const int o = kSegLd * (rg >> 2) + 4 * (rg & 3);
+                    const double2 u0 = *(const double2 *)&R0[o], u1 = *(const double2 *)&R0[o + 2];
+                    const double2 w0 = *(const double2 *)&R1[o], w1 = *(const double2 *)&R1[o + 2];
+                    ck[0] = u0.x; ck[1] = u0.y; ck[2] = u1.x; ck[3] = u1.y;
+                    cl[0] = w0.x; cl[1] = w0.y; cl[2] = w1.x; cl[3] = w1.y;
+                }
+                double fk[4], fl[4];  // -A(i,K) A_KK^-1 (rows K: A_KK^-1)
+                {
+                    const int r = rg_here();
 #pragma unroll
-                    for (int i = 0; i < 4; i++)
+                    for (int i = 0; i < 4; i++) {
+                        const bool piv = row_nat(r, i) < kp;
+                        const double a0 = piv ? -ck[i] : ck[i], a1 = piv ? -cl[i] : cl[i];
+                        fk[i] = -__builtin_fma(a0, ikk, a1 * ikl);
+                        fl[i] = -__builtin_fma(a0, ikl, a1 * ill);
+                    }
+                }
+                if (ownk) {  // row k <- ikk a_k. + ikl a_l. (the row restarts from 0)
+                    fk[rk] = ikk;
+                    fl[rk] = ikl;
 #pragma unroll
-                        for (int j = 0; j < 4; j++) Mb[i][4 * h + j] = __builtin_fma(nci[i], rj[j], Mb[i][4 * h + j]);
-#else
-                    Mb[h][h] += rj[h] * nci[h];
-#endif
-                    q0 = n0;
-                    q1 = n1;
+                    for (int j = 0; j < 16; j++) Mb[rk][j] = 0.0;
+                }
+                if (ownl) {  // row l <- ikl a_k. + ill a_l.
+                    fk[rl] = ikl;
+                    fl[rl] = ill;
+#pragma unroll
+                    for (int j = 0; j < 16; j++) Mb[rl][j] = 0.0;
+                }
+#pragma unroll
+                for (int h = 0; h < 8; h++) {  // 2-column chunks of both rows, the next one in flight
+                    double2 nk = qk, nl = ql;
+                    if (h < 7) {
+                        nk = k2[h + 1];
+                        nl = l2[h + 1];
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        Mb[i][2 * h] = __builtin_fma(fk[i], qk.x, __builtin_fma(fl[i], ql.x, Mb[i][2 * h]));
+                        Mb[i][2 * h + 1] = __builtin_fma(fk[i], qk.y, __builtin_fma(fl[i], ql.y, Mb[i][2 * h + 1]));
+                    }
+                    qk = nk;
+                    ql = nl;
                     // pin the updates here: sunk below the fix-up branches they would keep every
-                    // chunk of the row live (register budget)
+                    // chunk of the rows live (register budget)
 #pragma unroll
-                    for (int i = 0; i < 4; i++)
-#pragma unroll
-                        for (int j = 0; j < 4; j++) asm volatile("" : "+v"(Mb[i][4 * h + j]));
+                    for (int i = 0; i < 4; i++) asm volatile("" : "+v"(Mb[i][2 * h]), "+v"(Mb[i][2 * h + 1]));
                 }
-                if (coln) {
+                if (coln) {  // columns K: -A(i,K) A_KK^-1, rows K: A_KK^-1
 #pragma unroll
-                    for (int i = 0; i < 4; i++) Mb[i][kk] = nci[i];
-                    if (rown) Mb[rr][kk] = inv;
+                    for (int i = 0; i < 4; i++) {
+                        Mb[i][kk] = fk[i];
+                        Mb[i][kk + 1] = fl[i];
+                    }
+                    if (ownk) {
+                        Mb[rk][kk] = ikk;
+                        Mb[rk][kk + 1] = ikl;
+                    }
+                    if (ownl) {
+                        Mb[rl][kk] = ikl;
+                        Mb[rl][kk + 1] = ill;
+                    }
                 }
-#ifdef MPCQ_GJ_STAMPS
-                if (a.stamps && kp == 40 && (t == 0 || t == 80)) {
-                    double sum = 0.0;  // forces the FMAs to complete
-#pragma unroll
-                    for (int i = 0; i < 4; i++) sum += Mb[i][0] + Mb[i][15];
-                    a.stamps[(size_t)blockIdx.x * 8 + (t ? 6 : 3)] = __builtin_amdgcn_s_memtime() + (sum == 12345.0);
-                }
-                if (a.stamps && kp == 40 && t == 0) a.stamps[(size_t)blockIdx.x * 8 + 4] = __builtin_amdgcn_s_memtime();
-#endif
             }
         }
     };

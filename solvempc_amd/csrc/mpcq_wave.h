@@ -26,9 +26,11 @@ namespace mpcq {
 // read round trip: ~450 cycles of an ~1,800-cycle tail iteration.)
 __device__ __forceinline__ void wave_sync() { asm volatile("" ::: "memory"); }
 
+// full lane permutations only (quad_perm, row mirrors: every lane has a source), so no "old" operand:
+// the move needs no copy of v into its destination first
 template <int CTRL> __device__ __forceinline__ unsigned dpp_u(unsigned v)
 {
-    return (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false);
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
 }
 template <int CTRL> __device__ __forceinline__ float dpp_t(float v) { return __uint_as_float(dpp_u<CTRL>(__float_as_uint(v))); }
 template <int CTRL> __device__ __forceinline__ double dpp_t(double v)
