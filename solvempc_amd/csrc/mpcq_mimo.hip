@@ -574,6 +574,16 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
     __shared__ double s_D[kMimoN], s_E[kMimoN], s_K0[16], s_SW[32 * 16];  // D, E component-major
     __shared__ double s_xb[4][kMimoN];  // scan exchange buffers (rotated: a buffer is rewritten 4 barriers later)
     __shared__ double s_red[2][4][16];  // cross-wave reductions (alternating)
+    // the checks' settings and the cost scaling, read from LDS where they are used: held in SGPRs
+    // across the solve loop they spill into VGPR lanes that every iteration reloads
+    // (read back through readfirstlane: the branches on them, some holding barriers, stay uniform)
+    __shared__ double s_cfg[8];
+    auto cfg = [&](int i) {
+        const unsigned long long u = (unsigned long long)__double_as_longlong(s_cfg[i]);
+        const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)u);
+        const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(u >> 32));
+        return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+    };
     for (int i = t; i < kMimoN; i += kMimoThreads) {
         const int cc = i >> 5, kk = i & 31;
         const bool ok = cc < NU && kk < N;
@@ -590,7 +600,12 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
         s_SW[i] = (kk < N && ci < NU && cj < NU) ? ops[L.SW + (kk * NU + ci) * NU + cj] : 0.0;
     }
 
-    const double c64 = ops[L.cs], cinv = ops[L.cs + 1];
+    const double c64 = ops[L.cs];
+    if (t == 0) {
+        s_cfg[0] = st.eps_abs; s_cfg[1] = st.eps_rel; s_cfg[2] = st.eps_prim_inf; s_cfg[3] = st.eps_dual_inf;
+        s_cfg[4] = st.adaptive_rho_tolerance; s_cfg[5] = st.scaled_termination ? 1.0 : 0.0;
+        s_cfg[6] = c64; s_cfg[7] = ops[L.cs + 1];
+    }
     const double sigma = st.sigma, alpha = st.alpha, oma = 1.0 - st.alpha;
     const bool load = a.warm && !a.fresh;
 
@@ -759,6 +774,7 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
             const double xv = has_sol ? x * D : __builtin_nan("");
             if (a.x) a.x[(size_t)b * n + e] = xv;
             if (a.y) {
+                const double cinv = cfg(7);
                 a.y[(size_t)b * m + e] = has_sol ? (yt * E) * cinv : __builtin_nan("");
                 a.y[(size_t)b * m + n + e] = has_sol ? (yb * E) * cinv : __builtin_nan("");
             }
@@ -1124,7 +1140,8 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
             const double ax_z = v[0], ax_zs = v[1], zn_r = v[2], zn_s = v[3], axn_r = v[4], axn_s = v[5];
             const double dr_r = v[6], dr_s = v[7], qn_r = v[8], qn_s = v[9], atyn_r = v[10], atyn_s = v[11];
             const double pxn_r = v[12], pxn_s = v[13];
-            const bool scaled_term = st.scaled_termination != 0;
+            const double cinv = cfg(7);
+            const bool scaled_term = cfg(5) != 0.0;
             const double pri_res = scaled_term ? ax_z : ax_zs;
             const double dua_res = scaled_term ? dr_r : cinv * dr_s;
 
@@ -1152,7 +1169,7 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
                 w[2] = valid ? fabs(scaled_term ? vdpx : vdpx / D) : 0.0;          // |P^ dx|
                 block_reduce(w, 1u);
                 const double qdx = w[0], ndx = w[1], npdx = w[2];
-                const double cs = scaled_term ? 1.0 : c64;
+                const double cs = scaled_term ? 1.0 : cfg(6);
                 if (!(qdx < 0.0 && ndx > kDivisionTol && qdx < -cs * eps * ndx)) return false;
                 if (!(npdx < cs * eps * ndx)) return false;
                 const double adx = A_of(dx);
@@ -1167,16 +1184,16 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
             };
             auto check = [&](bool approx) -> int {
                 const double mul = approx ? 10.0 : 1.0;
-                const double ea = st.eps_abs * mul, er = st.eps_rel * mul;
+                const double ea = cfg(0) * mul, er = cfg(1) * mul;
                 if (pri_res > kInfty || dua_res > kInfty) return kNonCvx;
                 const double ep = ea + er * (scaled_term ? fmax(zn_r, axn_r) : fmax(zn_s, axn_s));
                 const double ed = ea + er * (scaled_term ? fmax(fmax(qn_r, atyn_r), pxn_r)
                                                          : cinv * fmax(fmax(qn_s, atyn_s), pxn_s));
                 const bool pok = pri_res < ep, dok = dua_res < ed;
                 if (pok && dok) return approx ? kSolvedInaccurate : kSolved;
-                if (!pok && primal_inf(st.eps_prim_inf * mul))
+                if (!pok && primal_inf(cfg(2) * mul))
                     return approx ? kPrimalInfeasibleInaccurate : kPrimalInfeasible;
-                if (!dok && dual_inf(st.eps_dual_inf * mul))
+                if (!dok && dual_inf(cfg(3) * mul))
                     return approx ? kDualInfeasibleInaccurate : kDualInfeasible;
                 return kUnsolved;
             };
@@ -1192,7 +1209,7 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
                         const double du = dr_r / (dn + kDivisionTol);
                         double rn = rho * sqrt(pr / (du + kDivisionTol));
                         rn = fmin(fmax(rn, kRhoMin), kRhoMax);
-                        if (rn > rho * st.adaptive_rho_tolerance || rn < rho / st.adaptive_rho_tolerance) {
+                        if (rn > rho * cfg(4) || rn < rho / cfg(4)) {
                             rho = fmin(fmax(rn, kRhoMin), kRhoMax);
                             ctl = 1;
                         }
