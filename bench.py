@@ -76,12 +76,13 @@ def parse(argv=None):
         a.dtype = {"cfg2": "mixed", "perplant": "f64", "stream": "f64"}.get(a.workload, "f32")
     if a.workload == "stream" and a.batch == 65536:
         a.batch = 4096
-    if a.workload == "perplant" and a.batch == 65536:
-        a.batch = 131072  # 1,048,576 / 8 GPUs
+    if a.workload == "perplant":
+        if a.batch == 65536:
+            a.batch = 131072  # 1,048,576 / 8 GPUs
+        if a.seed == 1:
+            a.seed = 2  # SURVEY §8d config 3 seed (weak and strong alike)
     if a.scaling == "strong" and not a.global_batch:
         a.global_batch = 1 << 20 if a.workload == "perplant" else a.batch  # BASELINE config 3: 1,048,576 plants
-        if a.seed == 1:
-            a.seed = 2  # SURVEY §8d config 3 seed
     if a.workload == "stream" and a.seed == 1:
         a.seed = 4  # SURVEY §8d config 5 seed
     if a.workload == "quadrotor":

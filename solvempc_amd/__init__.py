@@ -163,6 +163,13 @@ class BatchSolver:
         _capi.check(lib().mpcq_get_stream_path(self._ctx, C.byref(k)), "mpcq_get_stream_path")
         return ("graph", "wave", "tile")[k.value]
 
+    def order(self) -> tuple[bool, np.ndarray]:
+        """(whether the last solve ran hardest-first, its QPs per order bin: mpcq_get_order)."""
+        o, cnt = C.c_int(), np.zeros(64, dtype=np.int32)
+        _capi.check(lib().mpcq_get_order(self._ctx, C.byref(o), cnt.ctypes.data_as(C.POINTER(C.c_int))),
+                    "mpcq_get_order")
+        return bool(o.value), cnt
+
     def device_view(self) -> dict:
         v = _capi.DeviceView()
         _capi.check(lib().mpcq_device_view_get(self._ctx, C.byref(v)), "mpcq_device_view_get")

@@ -21,7 +21,7 @@ EXPORTS = (
     "mpcq_mpc_step", "mpcq_mpc_set_plant", "mpcq_mpc_simulate_device", "mpcq_mpc_run_device",
     "mpcq_condense", "mpcq_mpc_setup_plants_device", "mpcq_last_error", "mpcq_get_path",
     "mpcq_mimo_setup_plants_device", "mpcq_mimo_step_device", "mpcq_mpc_stream_counters",
-    "mpcq_mpc_plants_step_device", "mpcq_get_stream_path",
+    "mpcq_mpc_plants_step_device", "mpcq_get_stream_path", "mpcq_get_order",
 )
 
 
@@ -91,6 +91,7 @@ def lib() -> C.CDLL:
         "mpcq_mimo_step_device": (C.c_int, [vp, vp, vp, vp, vp]),
         "mpcq_get_path": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "mpcq_get_stream_path": (C.c_int, [vp, C.POINTER(C.c_int)]),
+        "mpcq_get_order": (C.c_int, [vp, C.POINTER(C.c_int), ip]),
         "mpcq_device_view_get": (C.c_int, [vp, C.POINTER(DeviceView)]),
         "mpcq_mpc_set_operators": (C.c_int, [vp, C.c_int, dp, dp, dp, dp, dp, dp]),
         "mpcq_mpc_step_device": (C.c_int, [vp, vp, vp, C.c_double, vp]),

@@ -137,6 +137,13 @@ struct mpcq_ctx {
     int *d_it_acc = nullptr, *d_uns_acc = nullptr;
     bool stream_acc = false;  // launches made inside mpcq_mpc_run_device accumulate into them
     int stream_path = MPCQ_STREAM_GRAPH;  // how the last mpcq_mpc_run_device call ran
+    // hardest-first order of a tile-path MPC step (mpcq_order.hip, build_order_map): the m x kStride
+    // violation map of plant 0, the bin counters and lists; ord_ok when the map matches the current setup
+    // and operators
+    double *d_ordmap = nullptr;
+    int *d_ord = nullptr;  // OrderBins::kBins counters, then kBins lists of `batch` entries
+    bool ord_ok = false;
+    bool ord_last = false;  // the last solve ran in that order (mpcq_get_order)
     // host copies of plant-0 scaling
     std::vector<double> hD, hE;
     double hc = 1.0;
@@ -295,7 +302,8 @@ int check_ctx(mpcq_ctx *c, Need need)
 // The plants' setup data and operator blocks (generic setups; mimo-only contexts keep one unused block)
 int ensure_plant_buffers(mpcq_ctx *c)
 {
-    if (c->d_ops) return MPCQ_OK;
+    // (no early return on one pointer: after a failed allocation the next call allocates whatever is still
+    // missing, so a call that returns MPCQ_OK always leaves every non-empty buffer allocated)
     const size_t Pg = c->mimo_only ? 1 : c->dims.n_plants, n = c->dims.n, m = c->dims.m;
     const mpcq::OpsLayout L = mpcq::OpsLayout::make(c->nc, c->mc);
     void **ptrs[] = {(void **)&c->d_P, (void **)&c->d_q0, (void **)&c->d_A, (void **)&c->d_l0, (void **)&c->d_u0,
@@ -468,7 +476,7 @@ int mpcq_destroy(mpcq_ctx *c)
                     c->d_xs, c->d_zs, c->d_ys, c->d_rhos, c->d_snx, c->d_sny, c->d_Fx, c->d_Fu, c->d_Fr,
                     c->d_Sbar, c->d_Ku, c->d_W0, c->d_X, c->d_U, c->d_img, c->d_list, c->d_counts,
                     c->d_itstate, c->d_Ad, c->d_Bd, c->d_step, c->d_flags, c->d_stamps, c->d_mimo,
-                    c->d_it_acc, c->d_uns_acc, c->d_Xs, c->d_Us};
+                    c->d_it_acc, c->d_uns_acc, c->d_Xs, c->d_Us, c->d_ordmap, c->d_ord};
     if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
     if (c->graph) (void)hipGraphDestroy(c->graph);
     for (void *p : ptrs)
@@ -597,6 +605,8 @@ int setup_on_device(mpcq_ctx *c, hipStream_t s)
     return reset_state(c, true);
 }
 
+static int build_order_map(mpcq_ctx *c);  // (below: the hardest-first order of a tile-path MPC step)
+
 int mpcq_setup(mpcq_ctx *c, const double *P, const double *q0, const double *A, const double *l0,
                const double *u0)
 {
@@ -622,6 +632,7 @@ int mpcq_setup(mpcq_ctx *c, const double *P, const double *q0, const double *A, 
     c->lower_free = lower_all_free(c, l0);
     c->gen++;
     c->mode = mpcq_ctx::Mode::Generic;
+    if ((rc = build_order_map(c))) return rc;  // (new P, A: the MPC step's order map, if operators are set)
     verbose_header(c, "mpcq_setup (osqp_setup: Ruiz scaling, constraint types, KKT basis)");
     return MPCQ_OK;
 }
@@ -707,7 +718,11 @@ int mpcq_warm_start(mpcq_ctx *c, const double *x, const double *y)
 // stops at 4 check_termination and runs the rest on tile waves.
 // *wave_tail: the last launch runs on the wave kernel (test hooks MPCQ_PHASES, MPCQ_TAIL=wave|tile).
 constexpr bool kWaveTail = false;  // [100, 125] + wave tail: slower in round 4 (tile tail f32 +2.4 %, mixed +8 %)
-static int phase_stops(const mpcq_settings &st, int batch, int cus, int *stops, bool *wave_tail)
+// ordered (phase 0 in hardest-first order, mpcq_order.hip): one launch per solve.  Its waves hold QPs of
+// like difficulty, so a re-pack saves little, and the slow QPs start first instead of waiting for a
+// later phase (config 2 mixed, one box: 0.335 ms against 0.406-0.416 ms for the same order with stops at
+// 100 or 125 and 0.446-0.474 ms in index order, profiles/r05a_order_mixed.log).
+static int phase_stops(const mpcq_settings &st, int batch, int cus, int *stops, bool *wave_tail, bool ordered = false)
 {
     const int ct = st.check_termination;
     int np = 0;
@@ -717,7 +732,9 @@ static int phase_stops(const mpcq_settings &st, int batch, int cus, int *stops, 
     int mult[kMaxPhases] = {3, 4};
     int nm = 2;
     *wave_tail = false;
-    if (!many && batch < 8192) {  // (a tile chain forced onto a small batch: one stop, tile waves)
+    if (ordered) {
+        nm = 0;
+    } else if (!many && batch < 8192) {  // (a tile chain forced onto a small batch: one stop, tile waves)
         mult[0] = 4;
         nm = 1;
     } else if (!many) {
@@ -776,7 +793,17 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
     const int B = c->dims.batch;
     int stops[kMaxPhases];
     bool wave_tail = false;
-    const int np = phase_stops(c->set, B, c->cus, stops, &wave_tail);
+    // an MPC step on the tile waves runs its batch hardest-first (mpcq_order.hip; test hook MPCQ_ORDER=0:
+    // index order)
+    const bool ordered = a.mpc && a.X && a.U && c->ord_ok && !wave_only && test_hook("MPCQ_ORDER")[0] != '0';
+    const int np = phase_stops(c->set, B, c->cus, stops, &wave_tail, ordered);
+    c->ord_last = ordered;
+    if (ordered) {
+        int *cnt = c->d_ord, *bins = c->d_ord + mpcq::OrderBins::kBins;
+        if (hipMemsetAsync(cnt, 0, 4 * (size_t)mpcq::OrderBins::kBins, s) != hipSuccess ||
+            mpcq_internal_order_bins(B, c->nx, c->dims.m, a.X, a.U, c->d_ordmap, a.xref, cnt, bins, B, s) != 0)
+            return -2;
+    }
     const int seg = mpcq::ListSeg::cap(B);
     const size_t lcap = (size_t)mpcq::ListSeg::kShards * seg;
     // Counter blocks: launch p zeroes block p + 1 (its successor's output) and a chain's final launch,
@@ -805,6 +832,9 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
         a.list_out = c->d_list + (size_t)((p + 1) % 2) * lcap;
         a.count_out = c->d_counts + (size_t)p * mpcq::ListSeg::kCounters;
         a.it_state = c->d_itstate;
+        a.ord_cnt = (ordered && p == 0) ? c->d_ord : nullptr;
+        a.ord_bins = (ordered && p == 0) ? c->d_ord + mpcq::OrderBins::kBins : nullptr;
+        a.ord_cap = B;
         a.stop_iter = stops[p];
         a.resume = p > 0;
         a.mpc = p == 0 ? mpc : 0;  // later phases read q, u from the buffers phase 0 filled
@@ -1022,15 +1052,22 @@ static void verbose_solve(mpcq_ctx *c, double seconds)
 
 extern "C" {
 
+static_assert(MPCQ_ORDER_BINS == mpcq::OrderBins::kBins, "mpcq_get_order's count array");
+
 static int launch_solve(mpcq_ctx *c, hipStream_t s, bool mpc, const double *X, double *U, double xref)
 {
     const auto t0 = std::chrono::steady_clock::now();
+    c->ord_last = false;  // (launch_phases sets it for a hardest-first tile solve)
     const int rc = c->dims.dtype == MPCQ_F32 ? launch_typed<float>(c, s, mpc, X, U, xref)
                                              : launch_typed<double>(c, s, mpc, X, U, xref);
     if (rc) return fail(MPCQ_ERR_HIP, std::string("ADMM kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
     c->last = s;
     c->fresh = false;
-    if (c->set.verbose) {
+    // settings.verbose: the summary needs the results on the host, so it synchronises the stream, which a
+    // stream under capture (mpcq_mpc_run_device's per-step graph) must not do: there the replay loop prints
+    // after each replayed step instead
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (c->set.verbose && hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
         (void)hipStreamSynchronize(s);
         verbose_solve(c, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     }
@@ -1104,6 +1141,20 @@ int mpcq_get_stream_path(mpcq_ctx *c, int *kind)
     return MPCQ_OK;
 }
 
+int mpcq_get_order(mpcq_ctx *c, int *ordered, int *counts)
+{
+    if (!c || !ordered) return fail(MPCQ_ERR_ARG, "null argument");
+    *ordered = c->ord_last ? 1 : 0;
+    if (counts) {
+        std::fill(counts, counts + mpcq::OrderBins::kBins, 0);
+        if (c->ord_last) {
+            HIPCHK(hipMemcpyAsync(counts, c->d_ord, 4 * (size_t)mpcq::OrderBins::kBins, hipMemcpyDeviceToHost, c->last));
+            HIPCHK(hipStreamSynchronize(c->last));
+        }
+    }
+    return MPCQ_OK;
+}
+
 int mpcq_get_path(mpcq_ctx *c, int *kind, int *paired)
 {
     if (!c) return fail(MPCQ_ERR_ARG, "null context");
@@ -1161,6 +1212,95 @@ static int materialize_qu(mpcq_ctx *c)
     return MPCQ_OK;
 }
 
+// The bound-violation map of the hardest-first order (mpcq_order.hip) for a shared plant with MPC
+// operators: x_u = -P^-1 q is the QP's unconstrained optimum and v = A x_u - u, with q = Fx X + Fu U +
+// (Fr 1) xref and u = W0 + Sbar X + Ku U (setF :372-375, setUpperBound :360-369), so
+//   v = (-A P^-1 Fx - Sbar) X + (-A P^-1 Fu - Ku) U + (-A P^-1 Fr 1) xref - W0   (OrderBins row layout).
+// Host fp64 (Cholesky of plant 0's P, upper triangle as OSQP reads it), once per setup / operator set;
+// the map only orders the batch (no result depends on it), so a P that is not positive definite or a
+// shape the kernel does not take just leaves the order off.
+static int build_order_map(mpcq_ctx *c)
+{
+    c->ord_ok = false;
+    const int n = c->dims.n, m = c->dims.m, nx = c->nx;
+    if (!c->tile || !c->mpc_ready || c->dims.n_plants != 1 || c->mode != mpcq_ctx::Mode::Generic || nx <= 0 ||
+        nx > 8 || m > mpcq::OrderBins::kMaxRows)
+        return MPCQ_OK;
+    std::vector<double> P((size_t)n * n), A((size_t)m * n), Fx((size_t)n * nx), Fu(n), Fr((size_t)n * n),
+        Sb((size_t)m * nx), Ku(m), W0(m);
+    hipStream_t s = c->last;
+    HIPCHK(hipMemcpyAsync(P.data(), c->d_P, 8 * P.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(A.data(), c->d_A, 8 * A.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(Fx.data(), c->d_Fx, 8 * Fx.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(Fu.data(), c->d_Fu, 8 * Fu.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(Fr.data(), c->d_Fr, 8 * Fr.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(Sb.data(), c->d_Sbar, 8 * Sb.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(Ku.data(), c->d_Ku, 8 * Ku.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(W0.data(), c->d_W0, 8 * W0.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    // Cholesky P = L L' (lower L in place, from P's upper triangle)
+    std::vector<double> L((size_t)n * n, 0.0);
+    for (int j = 0; j < n; j++) {
+        for (int i = j; i < n; i++) {
+            double v = P[(size_t)j * n + i];  // P(j, i), j <= i: upper triangle
+            for (int k = 0; k < j; k++) v -= L[(size_t)i * n + k] * L[(size_t)j * n + k];
+            if (i == j) {
+                if (!(v > 0.0)) return MPCQ_OK;  // not positive definite: no order
+                L[(size_t)j * n + j] = std::sqrt(v);
+            } else {
+                L[(size_t)i * n + j] = v / L[(size_t)j * n + j];
+            }
+        }
+    }
+    // Z = P^-1 [Fx Fu Fr1] (n x (nx + 2)), then the map rows
+    const int nr = nx + 2;
+    std::vector<double> Z((size_t)n * nr);
+    for (int i = 0; i < n; i++) {
+        for (int t = 0; t < nx; t++) Z[(size_t)i * nr + t] = Fx[(size_t)i * nx + t];
+        Z[(size_t)i * nr + nx] = Fu[i];
+        double fr = 0.0;
+        for (int t = 0; t < n; t++) fr += Fr[(size_t)i * n + t];
+        Z[(size_t)i * nr + nx + 1] = fr;
+    }
+    for (int r = 0; r < nr; r++) {
+        for (int i = 0; i < n; i++) {  // L y = b
+            double v = Z[(size_t)i * nr + r];
+            for (int k = 0; k < i; k++) v -= L[(size_t)i * n + k] * Z[(size_t)k * nr + r];
+            Z[(size_t)i * nr + r] = v / L[(size_t)i * n + i];
+        }
+        for (int i = n - 1; i >= 0; i--) {  // L' z = y
+            double v = Z[(size_t)i * nr + r];
+            for (int k = i + 1; k < n; k++) v -= L[(size_t)k * n + i] * Z[(size_t)k * nr + r];
+            Z[(size_t)i * nr + r] = v / L[(size_t)i * n + i];
+        }
+    }
+    constexpr int KS = mpcq::OrderBins::kStride;
+    std::vector<double> map((size_t)m * KS, 0.0);
+    for (int j = 0; j < m; j++) {
+        double az[10] = {0};
+        for (int r = 0; r < nr; r++)
+            for (int i = 0; i < n; i++) az[r] += A[(size_t)j * n + i] * Z[(size_t)i * nr + r];
+        double *row = map.data() + (size_t)j * KS;
+        for (int t = 0; t < nx; t++) row[t] = -az[t] - Sb[(size_t)j * nx + t];
+        row[8] = -az[nx] - Ku[j];
+        row[9] = -W0[j];
+        row[10] = -az[nx + 1];
+        for (int k = 0; k < KS; k++)
+            if (!std::isfinite(row[k])) return MPCQ_OK;
+    }
+    const size_t ord_ints = (size_t)mpcq::OrderBins::kBins * (1 + (size_t)c->dims.batch);
+    if (!c->d_ordmap && hipMalloc((void **)&c->d_ordmap, 8 * (size_t)mpcq::OrderBins::kMaxRows * KS) != hipSuccess)
+        return fail(MPCQ_ERR_HIP, "hipMalloc failed (order map)");
+    if (!c->d_ord) {
+        if (hipMalloc((void **)&c->d_ord, 4 * ord_ints) != hipSuccess) return fail(MPCQ_ERR_HIP, "hipMalloc failed (order lists)");
+        HIPCHK(hipMemsetAsync(c->d_ord, 0, 4 * ord_ints, s));  // (list entries are batch indices, from the start)
+        c->gen++;
+    }
+    if (int rc2 = h2d(c->d_ordmap, map.data(), 8 * map.size(), s)) return rc2;
+    c->ord_ok = true;
+    return MPCQ_OK;
+}
+
 int mpcq_mpc_set_operators(mpcq_ctx *c, int nx, const double *Fx, const double *Fu, const double *Fr,
                            const double *Sbar, const double *Ku, const double *W0)
 {
@@ -1179,7 +1319,7 @@ int mpcq_mpc_set_operators(mpcq_ctx *c, int nx, const double *Fx, const double *
         (rc = h2d(c->d_Ku, Ku, 8 * Pn * m, s)) || (rc = h2d(c->d_W0, W0, 8 * Pn * m, s)))
         return rc;
     c->mpc_ready = true;
-    return MPCQ_OK;
+    return build_order_map(c);
 }
 
 int mpcq_mpc_step_device(mpcq_ctx *c, const double *X, double *U, double xref, void *stream)
@@ -1404,8 +1544,14 @@ int mpcq_mpc_run_device(mpcq_ctx *c, double *X, double *U, double xref, int step
         c->gkey = {X, U, xref, noise_std, seed, first_qp, s, c->gen};
     }
     for (int k = done; k < steps; k++) {
+        const auto t0 = std::chrono::steady_clock::now();
         HIPCHK(hipGraphLaunch(c->gexec, s));
         if (sync_each && (rc = stage(("graph replay " + std::to_string(k)).c_str()))) return rc;
+        if (c->set.verbose) {  // (the captured solve printed nothing: launch_solve)
+            HIPCHK(hipStreamSynchronize(s));
+            c->last = s;
+            verbose_solve(c, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+        }
     }
     c->last = s;
     return MPCQ_OK;
@@ -1506,6 +1652,7 @@ int mpcq_mpc_setup_plants_device(mpcq_ctx *c, int nx, int s_rows, const double *
     c->gen++;
     c->mpc_ready = true;
     c->mode = mpcq_ctx::Mode::Generic;
+    if ((rc = build_order_map(c))) return rc;  // (a shared plant's tile path: the step's order map)
     verbose_header(c, "mpcq_mpc_setup_plants_device (condensing + osqp_setup per plant)");
     return MPCQ_OK;
 }
@@ -1559,7 +1706,7 @@ int mpcq_mimo_setup_plants_device(mpcq_ctx *c, int nx, int nu, int ny, int s_row
     if (nx <= 0 || nx > 12 || ny <= 0 || ny > 12 || s_rows < 0) return fail(MPCQ_ERR_ARG, "mimo: 1 <= n_x, n_y <= 12");
     if (n % nu || n / nu > 32 || n > 128 || m != 2 * n) return fail(MPCQ_ERR_ARG, "mimo: n = N n_u <= 128 (N <= 32), m = 2n");
     if (c->dims.n_plants != c->dims.batch || c->dims.dtype == MPCQ_F32)
-        return fail(MPCQ_ERR_ARG, "mimo: one plant per QP (n_plants == batch), dtype MPCQ_F64");
+        return fail(MPCQ_ERR_ARG, "mimo: one plant per QP (n_plants == batch), dtype MPCQ_F64 or MPCQ_F64_MIXED");
     if (!Ad || !Bd || !Cd || !Q || !R || !RD || !K || !K0 || !w0) return fail(MPCQ_ERR_ARG, "mimo: null plant array");
     const int N = n / nu;
     const mpcq::MimoLayout L = mpcq::MimoLayout::make(N, nx, nu, ny);

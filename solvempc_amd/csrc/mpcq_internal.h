@@ -133,6 +133,27 @@ struct ListSeg {
     __host__ __device__ static constexpr int cap(int batch) { return (batch + kShards - 1) / kShards + 256; }
 };
 
+// Hardest-first order of a shared-plant MPC step (mpcq_order.hip): the key v = max_j (A x_u - u)_j of a
+// QP (its unconstrained optimum's largest bound violation) falls in bin 2 log2|v| + 34 (two bins per
+// octave, 2^-16 .. 2^15.5, clamped), |v| = 0 in bin 0, a non-finite |v| in the last; the tile kernel's
+// phase 0 runs bin 0's QPs first.  The host's map (m rows of kStride doubles): v_j = r[0..nx) . X + r[8] U
+// + r[9] + r[10] xref.
+struct OrderBins {
+    static constexpr int kBins = 64;
+    static constexpr int kStride = 12;
+    static constexpr int kMaxRows = 64;
+    __host__ __device__ static int bin(double v)
+    {
+        const double a = v < 0.0 ? -v : v;
+        if (!(a < __builtin_inf())) return kBins - 1;  // inf, NaN
+        if (a == 0.0) return 0;
+        int e = 0;
+        const double f = __builtin_frexp(a, &e);  // a = f 2^e, f in [0.5, 1)
+        const int i = 2 * e + (f >= 0.70710678118654752 ? 1 : 0) + 32;
+        return i < 0 ? 0 : (i > kBins - 2 ? kBins - 2 : i);
+    }
+};
+
 // Arguments of the ADMM kernel (one QP per lane).
 // Persistent receding-horizon stream (config 5): control steps first_step .. first_step + steps - 1 of
 // the simulated plant X <- Ad X + Bd U + w (mpcq_plant_sim.h) between the solves.
@@ -190,6 +211,10 @@ struct AdmmArgs {
     int list_seg;               // ListSeg segment capacity
     int *it_state;              // [batch] iterations done so far in this solve
     int qp0;                    // QP index of identity-list slot 0 (sub-batch parts of a tile solve)
+    // phase 0 of a tile solve in hardest-first order (mpcq_order.hip; null: index order): OrderBins::kBins
+    // counts and the per-bin QP lists (bin k at ord_bins + k * ord_cap)
+    const int *ord_cnt, *ord_bins;
+    int ord_cap;
     int stop_iter;              // phase boundary (multiple of check_termination, or max_iter)
     int resume;                 // 1: phase >= 2 (state, rho and iteration count come from the buffers)
     long long *stamps;          // debug build (MPCQ_DEBUG_HOOKS): [wave][8] s_memtime stamps, or null
@@ -394,6 +419,10 @@ int mpcq_internal_front_end(int batch, int nx, int n, int m, const double *Xs, c
                             const double *Fx, const double *Fu, const double *Fr, const double *Sbar,
                             const double *Ku, const double *W0, double *q, double *u, hipStream_t s);
 int mpcq_internal_set_step(long long *step, long long v, hipStream_t s);
+// Hardest-first order of a shared-plant MPC step (mpcq_order.hip): per-QP bound-violation key from the
+// host's OrderBins map, scattered into OrderBins::kBins lists of capacity cap (cnt zero on entry).
+int mpcq_internal_order_bins(int batch, int nx, int m, const double *X, const double *U, const double *kmap,
+                             double xref, int *cnt, int *bins, int cap, hipStream_t s);
 // MIMO condensed MPC (mpcq_mimo.hip): per-plant condensing + Ruiz + P^, then the per-QP solve
 // (one 512-thread workgroup per QP: KKT inverse by Gauss-Jordan in VGPRs, structured A).
 int mpcq_internal_mimo_setup_launch(const mpcq::MimoSetupArgs *a, hipStream_t s);

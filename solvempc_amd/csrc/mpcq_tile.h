@@ -427,6 +427,21 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
         if (a.zero_cnt0) a.zero_cnt0[threadIdx.x * ListSeg::kStride] = 0;
     }
     if (blk * (refill ? WPB * a.sim.cpw : QPW) >= count) return;  // whole workgroup idle in this phase (uniform)
+    // phase 0 in hardest-first order (mpcq_order.hip): the prefix of the 64 bin counts, s_pref[k] = the
+    // first slot of bin k (one wave scans; read after the barrier below)
+    __shared__ int s_pref[OrderBins::kBins + 1];
+    const bool ordered = a.ord_cnt != nullptr && !seglist && !refill;
+    static_assert(OrderBins::kBins == 64, "one bin per lane of the scanning wave");
+    if (ordered && threadIdx.x < 64) {
+        int v = a.ord_cnt[threadIdx.x];
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int t = __shfl_up(v, d);
+            if ((int)threadIdx.x >= d) v += t;
+        }
+        s_pref[threadIdx.x + 1] = v;
+        if (threadIdx.x == 0) s_pref[0] = 0;
+    }
     for (int i = threadIdx.x; i < NCP; i += NTH) {
         s_lam[i] = a.ops.lam[i];
         s_D[i] = a.ops.D[i];
@@ -1839,7 +1854,18 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             const int slot = wave_slot + 16 * gi + c;
             valid[gi] = slot < count && (!refill || c < cpw);
             const int i = slot + (seglist ? seg * a.list_seg : 0);  // list entry
-            b_[gi] = valid[gi] ? (seglist ? a.list_in[i] : a.qp0 + i) : 0;
+            int qp = a.qp0 + i;
+            if (seglist) {
+                qp = a.list_in[i];
+            } else if (ordered) {  // slot -> bin k (s_pref[k] <= slot < s_pref[k + 1]) -> that bin's list
+                int k = 0;
+#pragma unroll
+                for (int st = 32; st; st >>= 1)
+                    if (s_pref[k + st] <= slot) k += st;
+                qp = a.ord_bins[(size_t)k * a.ord_cap + (slot - s_pref[k])];
+                qp = qp < 0 ? 0 : (qp >= a.batch ? a.batch - 1 : qp);  // (the lists hold batch indices only)
+            }
+            b_[gi] = valid[gi] ? qp : 0;
         }
         run_group(b_, valid);
     }

@@ -27,7 +27,10 @@ namespace mpcq {
 __device__ __forceinline__ void wave_sync() { asm volatile("" ::: "memory"); }
 
 // full lane permutations only (quad_perm, row mirrors: every lane has a source), so no "old" operand:
-// the move needs no copy of v into its destination first
+// the move needs no copy of v into its destination first.  bound_ctrl = true: a lane whose source lane is
+// inactive reads 0, so these moves (and wave_reduce / the scans built on them, here and in mpcq_mimo.hip /
+// mpcq_plant.hip) are only correct under a full EXEC mask.  Every caller runs them in wave-uniform control
+// flow (all 64 lanes active, dead lanes masked by value, not by EXEC).
 template <int CTRL> __device__ __forceinline__ unsigned dpp_u(unsigned v)
 {
     return (unsigned)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);

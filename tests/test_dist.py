@@ -138,3 +138,14 @@ def test_bench_under_torch_distributed_run():
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["steps"] == 4 and rec["warmup"] == 2
     assert rec["collective"] == {"backend": "gloo", "world_size": 2, "gathered": 1554, "matches_stream": True}
+
+
+def test_bench_parse_seed_per_workload_and_scaling():
+    """SURVEY §8d seeds: config 2 seed 1, config 3 (perplant) seed 2, config 4 (quadrotor) seed 3, config 5
+    (stream) seed 4, whatever the scaling mode; an explicit --seed always wins."""
+    parse = __import__("bench").parse
+    want = {"cfg2": 1, "perplant": 2, "quadrotor": 3, "stream": 4}
+    for wl, seed in want.items():
+        for sc in ("weak", "strong"):
+            assert parse(["--workload", wl, "--scaling", sc]).seed == seed, (wl, sc)
+            assert parse(["--workload", wl, "--scaling", sc, "--seed", "7"]).seed == 7, (wl, sc)

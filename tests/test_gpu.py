@@ -292,8 +292,9 @@ def test_full_batch_mpc_step_matches_oracle(plant, tail, monkeypatch):
     waves with the QPs past 125 iterations on the one-QP-per-wave kernel (MPCQ_TAIL=wave), whose
     front end rebuilds q, u from X, U (phase 0 saved those instead of q, u)."""
     import torch
-    if tail == "wave":
+    if tail == "wave":  # (index order: the hardest-first default runs one launch, no tail phase)
         monkeypatch.setenv("MPCQ_TAIL", "wave")
+        monkeypatch.setenv("MPCQ_ORDER", "0")
     N, B = 20, 65536
     ops, X, U, q, u = _problem(plant, N, B)
     l = np.full(2 * N, LMIN)
@@ -318,6 +319,7 @@ def test_full_batch_mpc_step_matches_oracle(plant, tail, monkeypatch):
         _osqp_terminated(x[off], s.dual()[off], q[off], u[off], ops)
     if tail == "wave":  # the variant ran its tail: QPs past 125 iterations exist (one QP per wave there)
         assert (it > 5 * 25).any()
+    assert s.order()[0] == (tail != "wave")  # the default ran the batch hardest-first (mpcq_order.hip)
     # the step's q, u as the solver keeps them (materialised from the saved X, U, after the tail's own
     # front end rebuilt them for its QPs) are the oracle's updateGradient / updateUpperBound data
     v = s.device_view()
@@ -1144,3 +1146,96 @@ def test_results_independent_of_batch_order(plant, dtype, monkeypatch):
     assert np.all(res[0][2] == sm.SOLVED)
     for a, b in zip(res[0], res[1]):
         assert np.array_equal(a, b)
+
+
+def test_verbose_stream_on_the_graph_path(plant, monkeypatch, capfd):
+    """settings.verbose (setVerbosity, ModelPredictiveControlAPI.cpp:51) on mpcq_mpc_run_device's per-step
+    graph path: the captured solve must not synchronise (that would invalidate the capture), so the summary
+    is printed after each replayed step instead: one OSQP-style summary per control step, results bit-identical
+    to the same stream without verbose."""
+    import torch
+    monkeypatch.setenv("MPCQ_STREAM", "graph")
+    N, B, steps = 20, 64, 5
+    ops = oracle.condense(plant, N)
+    l = np.full(2 * N, LMIN)
+    X, U = workload.stream_states(4, 0, B)
+
+    def run(verbose):
+        s = sm.BatchSolver(N, 2 * N, B, dtype="f64", settings=sm.default_settings(verbose=verbose))
+        s.setup(ops["P"], np.zeros(N), ops["A"], l, oracle.upper_bound(ops, np.zeros(4), 0.0))
+        s.mpc_set_operators(ops["Fx"], ops["Fu"], ops["Fr"], ops["Sbar"], ops["Ku"], ops["W0"])
+        s.mpc_set_plant(plant["Ad"], plant["Bd"])
+        Xd, Ud = torch.from_numpy(X.copy()).cuda(), torch.from_numpy(U.copy()).cuda()
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            s.mpc_run_device(Xd.data_ptr(), Ud.data_ptr(), 0.0, steps, 4, 0, 0, 1e-2, st.cuda_stream)
+        st.synchronize()
+        assert s.stream_path() == "graph"
+        return Xd.cpu().numpy(), Ud.cpu().numpy(), *s.info()
+
+    quiet = run(0)
+    capfd.readouterr()
+    loud = run(1)
+    out = capfd.readouterr().out
+    for a_, b_ in zip(quiet, loud):
+        assert np.array_equal(a_, b_)
+    assert out.count("libmpcq: batched OSQP-v0.6 ADMM") == 1
+    assert out.count("status:               solved") == steps, out[-2000:]
+    assert out.count("number of iterations:") == steps
+
+
+def _order_bin(v):
+    """OrderBins::bin (mpcq_internal.h) on the host: two bins per octave of |v|, 0 first, non-finite last."""
+    a = np.abs(v)
+    out = np.full(a.shape, 63, dtype=np.int64)
+    fin = np.isfinite(a)
+    f, e = np.frexp(a[fin])
+    i = np.clip(2 * e + (f >= 0.70710678118654752) + 32, 0, 62)
+    out[fin] = np.where(a[fin] == 0.0, 0, i)
+    return out
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64", "mixed"])
+def test_hardest_first_order_is_transparent(plant, dtype, monkeypatch):
+    """The tile path's hardest-first MPC step (mpcq_order.hip: the batch run in ascending |max_j (A x_u -
+    u)_j|, one launch) against the same step in index order with the phase chain (MPCQ_ORDER=0), on the
+    bench's 65,536 QPs: every output bit-identical (U, x, y, status, iterations, rho), since a QP's
+    arithmetic does not depend on its wave or launch.  The device's bins are the host's key binned the
+    same way (the key from x_u = -P^-1 q on the oracle's q, u, up to rounding at bin edges), and the
+    first bins hold the QPs that need the most iterations."""
+    import torch
+    N, B = 20, 65536
+    ops, X, U, q, u = _problem(plant, N, B)
+    l = np.full(2 * N, LMIN)
+
+    def run(order):
+        if order:
+            monkeypatch.delenv("MPCQ_ORDER", raising=False)
+        else:
+            monkeypatch.setenv("MPCQ_ORDER", "0")
+        s = sm.BatchSolver(N, 2 * N, B, dtype=dtype)
+        s.setup(ops["P"], np.zeros(N), ops["A"], l, oracle.upper_bound(ops, np.zeros(4), 0.0))
+        s.mpc_set_operators(ops["Fx"], ops["Fu"], ops["Fr"], ops["Sbar"], ops["Ku"], ops["W0"])
+        Xd, Ud = torch.from_numpy(X.copy()).cuda(), torch.from_numpy(U.copy()).cuda()
+        s.mpc_step_device(Xd.data_ptr(), Ud.data_ptr(), 0.0)
+        torch.cuda.synchronize()
+        o, cnt = s.order()
+        out = (Ud.cpu().numpy(), s.solution(), s.dual(), *s.info())
+        s.close()
+        return o, cnt, out
+
+    o1, cnt, got = run(True)
+    o0, cnt0, ref = run(False)
+    assert o1 and not o0 and cnt0.sum() == 0
+    for a_, b_ in zip(got, ref):
+        assert np.array_equal(a_, b_)
+    assert cnt.sum() == B
+    xu = -np.linalg.solve(ops["P"], q.T).T
+    key = (xu @ ops["A"].T - u).max(axis=1)
+    host = np.bincount(_order_bin(key), minlength=64)
+    assert np.abs(host - cnt).sum() <= 2e-3 * B, (host, cnt)
+    # the first ~1 % of the order holds the slowest QPs: every QP needing more than 125 iterations
+    it = ref[4]
+    first = np.cumsum(cnt) <= B // 100
+    slow_bins = _order_bin(key[it > 125])
+    assert first[slow_bins].all() or (it > 125).sum() == 0
