@@ -274,7 +274,7 @@ def main_quadrotor(a, rank, world, local, dist, dev):
     rec.update({
         # dominant stage: the per-QP solve (Gauss-Jordan KKT inverse + ADMM iterations, fp64 VALU)
         "roofline": {"bound": "valu", "achieved": tf(solve_flops, solve_ms), "peak": peak, "unit": "TFLOP/s",
-                     "frac": tf(solve_flops, solve_ms) / peak, "traffic": None,
+                     "frac": tf(solve_flops, solve_ms) / peak, "traffic": traffic_per_solve("quadrotor_f64", B, N),
                      "kernel": "mimo_solve_kernel (fp64 vector peak)", "kernel_ms": solve_ms,
                      "flops_per_step": solve_flops,
                      "flops_note": "algorithmic for the structured solve: 2n^3 per KKT inverse (1 + one per QP whose "
@@ -283,6 +283,7 @@ def main_quadrotor(a, rank, world, local, dist, dev):
         "stages": {"setup_ms": setup_ms, "solve_ms": solve_ms, "step_ms": kern_ms,
                    "setup_roofline": {"bound": "valu", "achieved": tf(setup_flops, setup_ms), "peak": peak,
                                       "unit": "TFLOP/s", "frac": tf(setup_flops, setup_ms) / peak,
+                                      "traffic": traffic_per_solve("quadrotor_setup_f64", B, N),
                                       "kernel": "mimo_setup_kernel", "flops_per_step": setup_flops,
                                       "note": "timed span includes the host read-back of the setup status word"}},
         "dense_equivalent": {"flops_per_step": dense, "achieved": tf(dense, kern_ms), "frac": tf(dense, kern_ms) / peak,
@@ -359,9 +360,11 @@ def _timed_loop(a, step, dist, world, dev):
     return wall, got
 
 
-def traffic_per_solve(dtype, batch, N):
-    """HBM bytes of one solve from the committed PMC pass (tools/pmc.sh -> profiles/), or None."""
-    f = ROOT / "profiles" / f"pmc_traffic_{dtype}.json"
+def traffic_per_solve(name, batch, N):
+    """HBM bytes of one bench step of the dominant kernel from the committed PMC pass of the same bench
+    command (tools/gpu_r05.sh pmc:<workload>,<dtype> -> tools/pmc_traffic.py -> profiles/pmc_traffic_<name>.json),
+    or None when no pass of this batch and horizon is committed."""
+    f = ROOT / "profiles" / f"pmc_traffic_{name}.json"
     try:
         d = json.loads(f.read_text())
     except (OSError, ValueError):
@@ -612,7 +615,8 @@ def main_lti(a, rank, world, local, dist, dev):
                   config)
     rec["roofline"] = {
         "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-        "frac": achieved / peak, "traffic": traffic_per_solve(a.dtype, B, N) if not stream_mode else None,
+        "frac": achieved / peak,
+        "traffic": traffic_per_solve(a.dtype if not stream_mode else f"stream_{a.dtype}", B, N),
         "mfma_util": mfma_util(a.dtype) if a.workload == "cfg2" and B == 65536 else None,
         "kernel": ({"tile": "admm_tile_kernel, stream mode (one launch: every plant's control steps and "
                             "plant updates, one plant per MFMA column)",
@@ -650,7 +654,7 @@ def main_lti(a, rank, world, local, dist, dev):
         pf = float(workload.flops_plant_step(N, 4, iters, refac, solver.settings.scaling, merged=merged).sum())
         ach = pf / (kern_ms * 1e-3) / 1e12
         rec["roofline"] = {"bound": "valu", "achieved": ach, "peak": peak, "unit": "TFLOP/s",
-                           "frac": ach / peak, "traffic": None,
+                           "frac": ach / peak, "traffic": traffic_per_solve(f"perplant_{a.dtype}", B, N),
                            "kernel": "plant_step_kernel (condense + setup + solve, one pass)", "kernel_ms": kern_ms,
                            "flops_per_step": pf,
                            "flops_note": "as performed (workload.flops_plant_step): condensing by lag scans, Ruiz, "

@@ -187,10 +187,9 @@ int mpcq_mpc_run_device(mpcq_ctx *ctx, double *X_dev, double *U_dev, double xref
 int mpcq_get_stream_path(mpcq_ctx *ctx, int *kind);
 /* Hardest-first order of the last solve (benchmarks and tests): *ordered = 1 when it was
  * a tile-path MPC step run in ascending |max_j (A x_u - u)_j| (x_u = -P^-1 q, the QP's unconstrained
- * optimum), else 0; counts (MPCQ_ORDER_BINS ints, or NULL) receives that step's QPs per bin (two bins per
- * octave of the key, bin 0 first; synchronises).  The order changes no result. */
-#define MPCQ_ORDER_BINS 64
-int mpcq_get_order(mpcq_ctx *ctx, int *ordered, int *counts);
+ * optimum; binned 16 per octave), else 0; order (batch ints, or NULL) receives that step's QPs in the
+ * order phase 0 ran them (synchronises).  The order changes no result. */
+int mpcq_get_order(mpcq_ctx *ctx, int *ordered, int *order);
 /* Per-QP counters of the last mpcq_mpc_run_device call (host arrays of `batch` ints, synchronises):
  * the ADMM iterations of all its control steps, and the steps whose solve did not end SOLVED
  * (controllerStep returning false, :102, where the reference's loop would exit, solver.cpp:50). */

@@ -164,11 +164,11 @@ class BatchSolver:
         return ("graph", "wave", "tile")[k.value]
 
     def order(self) -> tuple[bool, np.ndarray]:
-        """(whether the last solve ran hardest-first, its QPs per order bin: mpcq_get_order)."""
-        o, cnt = C.c_int(), np.zeros(64, dtype=np.int32)
-        _capi.check(lib().mpcq_get_order(self._ctx, C.byref(o), cnt.ctypes.data_as(C.POINTER(C.c_int))),
+        """(whether the last solve ran hardest-first, the QPs in the order phase 0 ran them: mpcq_get_order)."""
+        o, lst = C.c_int(), np.zeros(self.batch, dtype=np.int32)
+        _capi.check(lib().mpcq_get_order(self._ctx, C.byref(o), lst.ctypes.data_as(C.POINTER(C.c_int))),
                     "mpcq_get_order")
-        return bool(o.value), cnt
+        return bool(o.value), lst
 
     def device_view(self) -> dict:
         v = _capi.DeviceView()

@@ -144,10 +144,17 @@ struct mpcq_ctx {
     int *d_ord = nullptr;  // OrderBins::kBins counters, then kBins lists of `batch` entries
     bool ord_ok = false;
     bool ord_last = false;  // the last solve ran in that order (mpcq_get_order)
+    bool ord_clean = false;  // its bin counters are zero (an ordered phase-0 launch clears them)
+    // a tile solve whose finalize stored only the warm state (x', z, y) and U: d_x, d_y are formed from it by
+    // materialize_xy before anything reads them (get_solution / get_dual, the device view, verbose, or a
+    // call that overwrites the warm state)
+    bool xy_lazy = false;
     // host copies of plant-0 scaling
     std::vector<double> hD, hE;
     double hc = 1.0;
 };
+
+static int materialize_xy(mpcq_ctx *c);  // (below: the lazy x, y of a tile solve)
 
 namespace {
 
@@ -242,6 +249,7 @@ mpcq::AdmmArgs<T> make_args(mpcq_ctx *c)
 
 int reset_state(mpcq_ctx *c, bool reset_rho)
 {
+    if (int rc = materialize_xy(c)) return rc;  // (the warm state it zeroes is the last solve's x, y)
     const size_t B = c->dims.batch, es = c->dims.dtype == MPCQ_F32 ? 4 : 8;
     HIPCHK(hipMemsetAsync(c->d_xs, 0, es * c->nc * B, c->last));
     HIPCHK(hipMemsetAsync(c->d_zs, 0, es * c->mc * B, c->last));
@@ -514,6 +522,7 @@ static void dinf_bounds(mpcq_ctx *c, const double *blk, const mpcq::OpsLayout &L
 // readback.  One 4-byte flag word (non-convex plant, non-inequality row) comes back to the host.
 int setup_on_device(mpcq_ctx *c, hipStream_t s)
 {
+    if (int rc = materialize_xy(c)) return rc;  // (with the images of the solve that left it)
     c->qu_lazy = false;  // (q, u are re-broadcast from the setup data below)
     c->gen++;
     const size_t Pn = c->dims.n_plants, n = c->dims.n, m = c->dims.m, B = c->dims.batch;
@@ -686,6 +695,7 @@ int mpcq_cold_start(mpcq_ctx *c)
 
 int mpcq_warm_start(mpcq_ctx *c, const double *x, const double *y)
 {
+    c->xy_lazy = false;  // (x, y are staged in the output buffers below)
     int rc = check_ctx(c, kGeneric);
     if (rc) return rc;
     if (!x || (c->dims.m && !y)) return fail(MPCQ_ERR_ARG, "null x/y");
@@ -798,10 +808,12 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
     const bool ordered = a.mpc && a.X && a.U && c->ord_ok && !wave_only && test_hook("MPCQ_ORDER")[0] != '0';
     const int np = phase_stops(c->set, B, c->cus, stops, &wave_tail, ordered);
     c->ord_last = ordered;
+    int *const ord_cnt = c->d_ord, *const ord_key = c->d_ord + mpcq::OrderBins::kBins, *const ord_list = ord_key + B;
     if (ordered) {
-        int *cnt = c->d_ord, *bins = c->d_ord + mpcq::OrderBins::kBins;
-        if (hipMemsetAsync(cnt, 0, 4 * (size_t)mpcq::OrderBins::kBins, s) != hipSuccess ||
-            mpcq_internal_order_bins(B, c->nx, c->dims.m, a.X, a.U, c->d_ordmap, a.xref, cnt, bins, B, s) != 0)
+        // the counters are zero unless the last ordered sort's tile launch did not run (it clears them)
+        if (!c->ord_clean && hipMemsetAsync(ord_cnt, 0, 4 * (size_t)mpcq::OrderBins::kBins, s) != hipSuccess) return -2;
+        c->ord_clean = false;
+        if (mpcq_internal_order(B, c->nx, c->dims.m, a.X, a.U, c->d_ordmap, a.xref, ord_cnt, ord_key, ord_list, s) != 0)
             return -2;
     }
     const int seg = mpcq::ListSeg::cap(B);
@@ -817,6 +829,12 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
     const int tail_from = wave_only ? 0 : wave_tail ? np - 1 : kMaxPhases;
     int np_run = 0;
     a.list_seg = seg;
+    // a chain entirely on tile waves publishes x, y lazily (materialize_xy; test hook MPCQ_LAZY_XY=0: eager)
+    const bool lazy_xy = tail_from >= np && test_hook("MPCQ_LAZY_XY")[0] != '0';
+    if (lazy_xy) {
+        a.x = nullptr;
+        a.y = nullptr;
+    }
 
     // debug build: per-wave stage stamps of every phase launch, written to $MPCQ_TILE_STAMPS after the solve
     const char *stp = debug_hook("MPCQ_TILE_STAMPS");
@@ -832,9 +850,8 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
         a.list_out = c->d_list + (size_t)((p + 1) % 2) * lcap;
         a.count_out = c->d_counts + (size_t)p * mpcq::ListSeg::kCounters;
         a.it_state = c->d_itstate;
-        a.ord_cnt = (ordered && p == 0) ? c->d_ord : nullptr;
-        a.ord_bins = (ordered && p == 0) ? c->d_ord + mpcq::OrderBins::kBins : nullptr;
-        a.ord_cap = B;
+        a.ord_list = (ordered && p == 0) ? ord_list : nullptr;
+        a.ord_zero = (ordered && p == 0) ? ord_cnt : nullptr;
         a.stop_iter = stops[p];
         a.resume = p > 0;
         a.mpc = p == 0 ? mpc : 0;  // later phases read q, u from the buffers phase 0 filled
@@ -865,8 +882,10 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
                  : mpcq_internal_tile_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->KN, c->KM, s);
         if (rc) return rc;
         c->count0_clean = a.zero_cnt0 != nullptr;
+        if (a.ord_zero) c->ord_clean = true;
         np_run = p + 1;
     }
+    c->xy_lazy = lazy_xy;
     if (stp && *stp) {
         std::vector<long long> h(8 * waves * kMaxPhases);
         if (hipMemcpyAsync(h.data(), c->d_stamps, 8 * h.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -992,7 +1011,7 @@ static void verbose_solve(mpcq_ctx *c, double seconds)
     const size_t B = c->dims.batch, n = c->dims.n, m = c->dims.m;
     std::vector<int> st(B), it(B);
     std::vector<double> rho(B), x(n), y(m), q(n), u(m), l(m), P(n * n), A(m * n);
-    if (hipStreamSynchronize(c->last) != hipSuccess ||
+    if (materialize_xy(c) != MPCQ_OK || hipStreamSynchronize(c->last) != hipSuccess ||
         hipMemcpy(st.data(), c->d_status, 4 * B, hipMemcpyDeviceToHost) != hipSuccess ||
         hipMemcpy(it.data(), c->d_iter, 4 * B, hipMemcpyDeviceToHost) != hipSuccess ||
         hipMemcpy(rho.data(), c->d_rho, 8 * B, hipMemcpyDeviceToHost) != hipSuccess ||
@@ -1052,12 +1071,11 @@ static void verbose_solve(mpcq_ctx *c, double seconds)
 
 extern "C" {
 
-static_assert(MPCQ_ORDER_BINS == mpcq::OrderBins::kBins, "mpcq_get_order's count array");
-
 static int launch_solve(mpcq_ctx *c, hipStream_t s, bool mpc, const double *X, double *U, double xref)
 {
     const auto t0 = std::chrono::steady_clock::now();
     c->ord_last = false;  // (launch_phases sets it for a hardest-first tile solve)
+    c->xy_lazy = false;   // (and this, for a chain that publishes x, y lazily)
     const int rc = c->dims.dtype == MPCQ_F32 ? launch_typed<float>(c, s, mpc, X, U, xref)
                                              : launch_typed<double>(c, s, mpc, X, U, xref);
     if (rc) return fail(MPCQ_ERR_HIP, std::string("ADMM kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
@@ -1103,6 +1121,7 @@ int mpcq_get_solution(mpcq_ctx *c, double *x)
     int rc = check_ctx(c, kAnySetup);
     if (rc) return rc;
     if (!x) return fail(MPCQ_ERR_ARG, "null x");
+    if ((rc = materialize_xy(c))) return rc;
     return d2h(c, x, c->d_x, 8 * (size_t)c->dims.batch * c->dims.n);
 }
 
@@ -1111,6 +1130,7 @@ int mpcq_get_dual(mpcq_ctx *c, double *y)
     int rc = check_ctx(c, kAnySetup);
     if (rc) return rc;
     if (!y && c->dims.m) return fail(MPCQ_ERR_ARG, "null y");
+    if ((rc = materialize_xy(c))) return rc;
     return d2h(c, y, c->d_y, 8 * (size_t)c->dims.batch * c->dims.m);
 }
 
@@ -1141,14 +1161,16 @@ int mpcq_get_stream_path(mpcq_ctx *c, int *kind)
     return MPCQ_OK;
 }
 
-int mpcq_get_order(mpcq_ctx *c, int *ordered, int *counts)
+int mpcq_get_order(mpcq_ctx *c, int *ordered, int *order)
 {
     if (!c || !ordered) return fail(MPCQ_ERR_ARG, "null argument");
     *ordered = c->ord_last ? 1 : 0;
-    if (counts) {
-        std::fill(counts, counts + mpcq::OrderBins::kBins, 0);
-        if (c->ord_last) {
-            HIPCHK(hipMemcpyAsync(counts, c->d_ord, 4 * (size_t)mpcq::OrderBins::kBins, hipMemcpyDeviceToHost, c->last));
+    if (order) {
+        const size_t B = c->dims.batch;
+        if (!c->ord_last) {
+            for (size_t i = 0; i < B; i++) order[i] = (int)i;
+        } else {
+            HIPCHK(hipMemcpyAsync(order, c->d_ord + mpcq::OrderBins::kBins + B, 4 * B, hipMemcpyDeviceToHost, c->last));
             HIPCHK(hipStreamSynchronize(c->last));
         }
     }
@@ -1167,8 +1189,8 @@ int mpcq_get_path(mpcq_ctx *c, int *kind, int *paired)
 int mpcq_device_view_get(mpcq_ctx *c, mpcq_device_view *v)
 {
     if (!c || !v) return fail(MPCQ_ERR_ARG, "null argument");
-    const int rc = materialize_qu(c);  // (enqueued on the context's last stream)
-    if (rc) return rc;
+    int rc = materialize_qu(c);  // (enqueued on the context's last stream)
+    if (rc || (rc = materialize_xy(c))) return rc;
     v->q = c->d_q;
     v->u = c->d_u;
     v->l = c->d_l;
@@ -1210,6 +1232,24 @@ static int materialize_qu(mpcq_ctx *c)
                                 c->d_u, c->last) != 0)
         return fail(MPCQ_ERR_HIP, "front-end kernel launch failed");
     return MPCQ_OK;
+}
+
+// d_x, d_y of the last tile solve from its stored warm state (mpcq_tile.h tile_publish_kernel), once.
+static int materialize_xy(mpcq_ctx *c)
+{
+    if (!c->xy_lazy) return MPCQ_OK;
+    c->xy_lazy = false;
+    int rc;
+    if (c->dims.dtype == MPCQ_F32) {
+        auto a = make_args<float>(c);
+        a.img = (const float *)c->d_img;
+        rc = mpcq_internal_tile_publish_f32(&a, c->KN, c->KM, a.paired = c->paired && c->all_ineq && c->lower_free, c->last);
+    } else {
+        auto a = make_args<double>(c);
+        a.img = (const double *)c->d_img;
+        rc = mpcq_internal_tile_publish_f64(&a, c->KN, c->KM, a.paired = c->paired && c->all_ineq && c->lower_free, c->last);
+    }
+    return rc ? fail(MPCQ_ERR_HIP, "solution publish kernel failed") : MPCQ_OK;
 }
 
 // The bound-violation map of the hardest-first order (mpcq_order.hip) for a shared plant with MPC
@@ -1288,12 +1328,13 @@ static int build_order_map(mpcq_ctx *c)
         for (int k = 0; k < KS; k++)
             if (!std::isfinite(row[k])) return MPCQ_OK;
     }
-    const size_t ord_ints = (size_t)mpcq::OrderBins::kBins * (1 + (size_t)c->dims.batch);
+    const size_t ord_ints = (size_t)mpcq::OrderBins::kBins + 2 * (size_t)c->dims.batch;  // counters, keys, list
     if (!c->d_ordmap && hipMalloc((void **)&c->d_ordmap, 8 * (size_t)mpcq::OrderBins::kMaxRows * KS) != hipSuccess)
         return fail(MPCQ_ERR_HIP, "hipMalloc failed (order map)");
     if (!c->d_ord) {
         if (hipMalloc((void **)&c->d_ord, 4 * ord_ints) != hipSuccess) return fail(MPCQ_ERR_HIP, "hipMalloc failed (order lists)");
         HIPCHK(hipMemsetAsync(c->d_ord, 0, 4 * ord_ints, s));  // (list entries are batch indices, from the start)
+        c->ord_clean = true;
         c->gen++;
     }
     if (int rc2 = h2d(c->d_ordmap, map.data(), 8 * map.size(), s)) return rc2;
@@ -1395,6 +1436,7 @@ int mpcq_mpc_simulate_device(mpcq_ctx *c, double *X, const double *U, unsigned l
 template <typename T>
 static int launch_stream(mpcq_ctx *c, hipStream_t s, double *X, double *U, double xref, const mpcq::StreamArgs &sa)
 {
+    c->xy_lazy = false;  // (the stream writes every QP's x, y at its last step)
     auto a = make_args<T>(c);
     a.mpc = 1; a.mpc_u = 1; a.nx = c->nx; a.X = X; a.U = U; a.xref = xref;
     a.Fx = c->d_Fx; a.Fu = c->d_Fu; a.Fr = c->d_Fr; a.Sbar = c->d_Sbar; a.Ku = c->d_Ku; a.W0 = c->d_W0;
@@ -1417,6 +1459,7 @@ extern "C" {
 template <typename T>
 static int launch_tile_stream(mpcq_ctx *c, hipStream_t s, double *X, double *U, double xref, mpcq::StreamArgs sa)
 {
+    c->xy_lazy = false;  // (the stream writes every QP's x, y at its last step)
     const mpcq_settings &st = c->set;
     const int ct = st.check_termination;
     auto a = make_args<T>(c);
@@ -1664,6 +1707,7 @@ int mpcq_mpc_plants_step_device(mpcq_ctx *c, int nx, int s_rows, const double *A
 {
     int rc = check_generic_dims(c);
     if (rc) return rc;
+    if ((rc = materialize_xy(c))) return rc;  // (a pending lazy x, y first: the kernel below rewrites the state)
     const int n = c->dims.n, m = c->dims.m;
     if (nx <= 0 || nx > 8 || s_rows < 0) return fail(MPCQ_ERR_ARG, "plants_step: 1 <= nx <= 8, s_rows >= 0");
     if (m != 2 * n || n > 32) return fail(MPCQ_ERR_ARG, "plants_step: n = N <= 32, m = 2N (ModelPredictiveControlAPI.cpp:47-48)");
@@ -1701,6 +1745,7 @@ int mpcq_mimo_setup_plants_device(mpcq_ctx *c, int nx, int nu, int ny, int s_row
 {
     int rc = check_ctx(c, kNone);
     if (rc) return rc;
+    if ((rc = materialize_xy(c))) return rc;  // (the operator blocks below replace the tile images' role)
     const int n = c->dims.n, m = c->dims.m;
     if (nu != 1 && nu != 2 && nu != 4) return fail(MPCQ_ERR_ARG, "mimo: n_u must be 1, 2 or 4");
     if (nx <= 0 || nx > 12 || ny <= 0 || ny > 12 || s_rows < 0) return fail(MPCQ_ERR_ARG, "mimo: 1 <= n_x, n_y <= 12");
@@ -1766,6 +1811,7 @@ int mpcq_mimo_step_device(mpcq_ctx *c, const double *X, double *U, const double 
 {
     int rc = check_ctx(c, kNone);
     if (rc) return rc;
+    if ((rc = materialize_xy(c))) return rc;  // (a pending lazy x, y first: the kernel below rewrites the state)
     if (c->mode != mpcq_ctx::Mode::Mimo) return fail(MPCQ_ERR_ORDER, "mpcq_mimo_setup_plants_device has not succeeded");
     if (!X || !U) return fail(MPCQ_ERR_ARG, "null X/U");
     mpcq::MimoArgs a{};

@@ -134,12 +134,14 @@ struct ListSeg {
 };
 
 // Hardest-first order of a shared-plant MPC step (mpcq_order.hip): the key v = max_j (A x_u - u)_j of a
-// QP (its unconstrained optimum's largest bound violation) falls in bin 2 log2|v| + 34 (two bins per
-// octave, 2^-16 .. 2^15.5, clamped), |v| = 0 in bin 0, a non-finite |v| in the last; the tile kernel's
-// phase 0 runs bin 0's QPs first.  The host's map (m rows of kStride doubles): v_j = r[0..nx) . X + r[8] U
-// + r[9] + r[10] xref.
+// QP (its unconstrained optimum's largest bound violation) falls in bin floor(16 log2|v|) + 256 (16 bins
+// per octave, 2^-16 .. 2^16, clamped), |v| = 0 in bin 0, a non-finite |v| in the last; phase 0 runs bin
+// 0's QPs first.  The host's map (m rows of kStride doubles): v_j = r[0..nx) . X + r[8] U + r[9] +
+// r[10] xref.  A QP's rank inside its bin takes the low kRankBits of its key word.
 struct OrderBins {
-    static constexpr int kBins = 64;
+    static constexpr int kBins = 512;
+    static constexpr int kPerOctave = 16;
+    static constexpr int kRankBits = 22;  // batches below 4,194,304 QPs
     static constexpr int kStride = 12;
     static constexpr int kMaxRows = 64;
     __host__ __device__ static int bin(double v)
@@ -148,8 +150,11 @@ struct OrderBins {
         if (!(a < __builtin_inf())) return kBins - 1;  // inf, NaN
         if (a == 0.0) return 0;
         int e = 0;
-        const double f = __builtin_frexp(a, &e);  // a = f 2^e, f in [0.5, 1)
-        const int i = 2 * e + (f >= 0.70710678118654752 ? 1 : 0) + 32;
+        const double f = __builtin_frexp(a, &e);  // a = f 2^e, f in [0.5, 1): log2 a = e - 1 + log2(2 f)
+        // the fraction's 16 sub-octave steps from its top mantissa bits (a monotone map of a within the
+        // octave: ordering only needs monotone bins, not exact logarithms)
+        const int sub = (int)((f - 0.5) * 32.0);  // 0 .. 15
+        const int i = (e - 1) * kPerOctave + sub + kBins / 2;
         return i < 0 ? 0 : (i > kBins - 2 ? kBins - 2 : i);
     }
 };
@@ -211,10 +216,10 @@ struct AdmmArgs {
     int list_seg;               // ListSeg segment capacity
     int *it_state;              // [batch] iterations done so far in this solve
     int qp0;                    // QP index of identity-list slot 0 (sub-batch parts of a tile solve)
-    // phase 0 of a tile solve in hardest-first order (mpcq_order.hip; null: index order): OrderBins::kBins
-    // counts and the per-bin QP lists (bin k at ord_bins + k * ord_cap)
-    const int *ord_cnt, *ord_bins;
-    int ord_cap;
+    // phase 0 of a tile solve in hardest-first order (mpcq_order.hip; null: index order): slot i runs QP
+    // ord_list[i]; workgroup 0 zeroes the OrderBins::kBins counters ord_zero for the next solve
+    const int *ord_list;
+    int *ord_zero;
     int stop_iter;              // phase boundary (multiple of check_termination, or max_iter)
     int resume;                 // 1: phase >= 2 (state, rho and iteration count come from the buffers)
     long long *stamps;          // debug build (MPCQ_DEBUG_HOOKS): [wave][8] s_memtime stamps, or null
@@ -396,6 +401,9 @@ int mpcq_internal_warm_f32(const mpcq::AdmmArgs<float> *a, int nc, int mc, const
 int mpcq_internal_tile_supported(int KN, int KM);
 int mpcq_internal_tile_launch_f64(const mpcq::AdmmArgs<double> *a, int KN, int KM, hipStream_t s);
 int mpcq_internal_tile_launch_f32(const mpcq::AdmmArgs<float> *a, int KN, int KM, hipStream_t s);
+// The lazily published x, y of the last tile solve from its stored warm state (mpcq_tile.h tile_publish_kernel).
+int mpcq_internal_tile_publish_f64(const mpcq::AdmmArgs<double> *a, int KN, int KM, int paired, hipStream_t s);
+int mpcq_internal_tile_publish_f32(const mpcq::AdmmArgs<float> *a, int KN, int KM, int paired, hipStream_t s);
 // The receding-horizon stream in one tile launch (AdmmArgs::sim; every column one plant through all its
 // control steps).  0 launched, -1 not the paired condensed-MPC shape.
 int mpcq_internal_tile_stream_launch_f64(const mpcq::AdmmArgs<double> *a, int KN, int KM, hipStream_t s);
@@ -420,9 +428,9 @@ int mpcq_internal_front_end(int batch, int nx, int n, int m, const double *Xs, c
                             const double *Ku, const double *W0, double *q, double *u, hipStream_t s);
 int mpcq_internal_set_step(long long *step, long long v, hipStream_t s);
 // Hardest-first order of a shared-plant MPC step (mpcq_order.hip): per-QP bound-violation key from the
-// host's OrderBins map, scattered into OrderBins::kBins lists of capacity cap (cnt zero on entry).
-int mpcq_internal_order_bins(int batch, int nx, int m, const double *X, const double *U, const double *kmap,
-                             double xref, int *cnt, int *bins, int cap, hipStream_t s);
+// host's OrderBins map, counting-sorted into list (cnt: OrderBins::kBins counters, zero on entry).
+int mpcq_internal_order(int batch, int nx, int m, const double *X, const double *U, const double *kmap, double xref,
+                        int *cnt, int *key, int *list, hipStream_t s);
 // MIMO condensed MPC (mpcq_mimo.hip): per-plant condensing + Ruiz + P^, then the per-QP solve
 // (one 512-thread workgroup per QP: KKT inverse by Gauss-Jordan in VGPRs, structured A).
 int mpcq_internal_mimo_setup_launch(const mpcq::MimoSetupArgs *a, hipStream_t s);

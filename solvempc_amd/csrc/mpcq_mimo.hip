@@ -74,21 +74,39 @@ __device__ __forceinline__ double lane_suffix_max(double v, int lane)
 }
 
 // ----------------------------------------------------------------------------------------------
-// setup: one 1024-thread workgroup (16 waves) per plant; LDS carve (doubles).  P (n x (n+1)) is the
-// big region; before P is built it holds the history QCA_d = Q Cd Ad^(d+1) of the recurrences.
+// setup: one 1024-thread workgroup (16 waves) per plant, two plants per CU; LDS carve (doubles), under
+// 80 KiB per plant for config 4 (n 120).  P is symmetric and kept as its packed upper triangle (row i holds
+// columns i .. n-1 at i n - i (i - 1) / 2), the diagonal nu x nu blocks of its construction in full (Dblk).
+// Regions are shared by lifetime: X holds the recurrences' histories (QCA_d = Q Cd Ad^(d+1), Ad^d Bd, the
+// powers Ad^1..Ad^4, then the Fx partial tiles) until P is built there, and after the last scan the Ruiz
+// scalings D~, E~ take Dblk's place; Y holds CS until P is complete, then the Ruiz column partials.
 struct MimoSetupShape {
-    int N, nx, nu, ny, n, ldp;
-    size_t hist, P, Ad, Bd, Cd, Q, R, RD, K0, AB, CA, CS, QCS, Dv, Ev, Dt, Et, cm, wk, red, sh, total;
+    int N, nx, nu, ny, n, np;
+    size_t P, Dblk, QCAh, ABh, Pw4, part, Dt, Et, CS, cm, wk;
+    size_t Ad, Bd, Cd, Q, R, RD, K0, CA, Dv, Ev, red, sh, total;
+    __host__ __device__ static size_t mx(size_t a, size_t b) { return a > b ? a : b; }
     __host__ __device__ static MimoSetupShape make(int N, int nx, int nu, int ny)
     {
         MimoSetupShape s{};
         s.N = N; s.nx = nx; s.nu = nu; s.ny = ny; s.n = N * nu;
-        s.ldp = s.n + 1;  // odd stride: column walks by consecutive lanes hit distinct banks
-        size_t o = 0;
-        // powers, QCA and Ad^d Bd histories, then the Fx partial tiles ((n+15)/16 x 256)
-        s.hist = (size_t)N * (nx * nx + ny * nx + nx * nu);
-        const size_t scratch = s.hist + (size_t)((s.n + 15) / 16) * 256;
-        s.P = o; o += (size_t)s.n * s.ldp > scratch ? (size_t)s.n * s.ldp : scratch;
+        s.np = s.n * (s.n + 1) / 2;
+        // region X
+        s.QCAh = 0;
+        s.ABh = s.QCAh + (size_t)N * ny * nx;
+        s.Pw4 = s.ABh + (size_t)N * nx * nu;
+        s.part = s.ABh;  // (Fx partial tiles: after the recurrences, over AB_d and the powers)
+        const size_t xa = s.ABh + mx((size_t)N * nx * nu + (size_t)4 * nx * nx, (size_t)((s.n + 15) / 16) * 256);
+        s.P = 0;
+        s.Dblk = s.np;
+        s.Dt = s.np;      // (after the scans: D~, E~ of the Ruiz passes where Dblk was)
+        s.Et = s.np + s.n;
+        const size_t xb = s.np + mx((size_t)N * nu * nu, (size_t)2 * s.n);
+        size_t o = mx(xa, xb);
+        // region Y
+        s.CS = o;
+        s.cm = o;         // (column-max partials, 8 row slices, once CS is dead)
+        s.wk = o + 8 * 128;  // (A-norm block maxima, columns and rows)
+        o += mx((size_t)N * ny * nu, (size_t)8 * 128 + 2 * 32 * 4);
         s.Ad = o; o += (size_t)nx * nx;
         s.Bd = o; o += (size_t)nx * nu;
         s.Cd = o; o += (size_t)ny * nx;
@@ -96,22 +114,18 @@ struct MimoSetupShape {
         s.R = o; o += (size_t)nu * nu;
         s.RD = o; o += (size_t)nu * nu;
         s.K0 = o; o += (size_t)nu * nu;
-        s.AB = o; o += (size_t)2 * nx * nu;  // double-buffered recurrences
-        s.CA = o; o += (size_t)2 * ny * nx;
-        s.CS = o; o += (size_t)N * ny * nu;
-        s.QCS = o; o += (size_t)N * ny * nu;
+        s.CA = o; o += (size_t)ny * nx;
         s.Dv = o; o += s.n;
         s.Ev = o; o += s.n;
-        s.Dt = o; o += s.n;
-        s.Et = o; o += s.n;
-        s.cm = o; o += (size_t)8 * 128;  // column-max partials (8 row slices)
-        s.wk = o; o += (size_t)2 * 32 * 4;  // A-norm block maxima (columns, rows)
         s.red = o; o += 16;
         s.sh = o; o += 8;
         s.total = o;
         return s;
     }
 };
+// packed upper-triangle index of P(i, j), i <= j
+__device__ __forceinline__ int pk_up(int i, int j, int n) { return i * n - (i * (i - 1)) / 2 + (j - i); }
+__device__ __forceinline__ int pk(int i, int j, int n) { return i <= j ? pk_up(i, j, n) : pk_up(j, i, n); }
 
 constexpr int kMimoSetupThreads = 1024;
 
@@ -127,7 +141,7 @@ __device__ __forceinline__ double dot12(const double *a, int sa, const double *b
     return s0 + s1;
 }
 
-__global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetupArgs a)
+__global__ __launch_bounds__(kMimoSetupThreads, 8) void mimo_setup_kernel(MimoSetupArgs a)
 {
     extern __shared__ double sm[];
     const int pl = blockIdx.x;
@@ -136,9 +150,9 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
     constexpr int T = kMimoSetupThreads;
     const int N = a.N, nx = a.nx, nu = a.nu, ny = a.ny;
     const MimoSetupShape S = MimoSetupShape::make(N, nx, nu, ny);
-    const int n = S.n, ldp = S.ldp;
-    double *P = sm + S.P, *Ad = sm + S.Ad, *Bd = sm + S.Bd, *Cd = sm + S.Cd, *Q = sm + S.Q, *R = sm + S.R;
-    double *RD = sm + S.RD, *K0 = sm + S.K0, *AB = sm + S.AB, *CA = sm + S.CA, *CS = sm + S.CS, *QCS = sm + S.QCS;
+    const int n = S.n;
+    double *P = sm + S.P, *Dblk = sm + S.Dblk, *Ad = sm + S.Ad, *Bd = sm + S.Bd, *Cd = sm + S.Cd, *Q = sm + S.Q;
+    double *R = sm + S.R, *RD = sm + S.RD, *K0 = sm + S.K0, *CA = sm + S.CA, *CS = sm + S.CS;
     double *Dv = sm + S.Dv, *Ev = sm + S.Ev, *Dt = sm + S.Dt, *Et = sm + S.Et, *cm = sm + S.cm, *wk = sm + S.wk;
     double *red = sm + S.red;
     const MimoLayout L = MimoLayout::make(N, nx, nu, ny);
@@ -151,7 +165,7 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
 
     // ---- plant data -> LDS
     for (int e = t; e < nx * nx; e += T) Ad[e] = a.Ad[(size_t)pl * nx * nx + e];
-    for (int e = t; e < nx * nu; e += T) Bd[e] = AB[e] = a.Bd[(size_t)pl * nx * nu + e];
+    for (int e = t; e < nx * nu; e += T) Bd[e] = a.Bd[(size_t)pl * nx * nu + e];
     for (int e = t; e < ny * nx; e += T) Cd[e] = a.Cd[(size_t)pl * ny * nx + e];
     for (int e = t; e < ny * ny; e += T) Q[e] = a.Q[(size_t)pl * ny * ny + e];
     for (int e = t; e < nu * nu; e += T) {
@@ -166,38 +180,41 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
     MPCQ_SSTAMP(1);
 
     // ---- setTransformations (:187-204): CS_d = sum_{k<=d} Cd Ad^k Bd (the distinct blocks of Su) and
-    // QCA_d = Q Cd Ad^(d+1) (for Fx = 2 (Sx' Qbar Su)', :307).  The powers Ad^k (k <= N) by doubling
-    // (log2 N barriers instead of one per horizon step), then every product of a horizon step at once.
-    double *Pw = P;                                     // Ad^k at Pw + (k-1) nx^2, k = 1..N
-    double *QCAh = P + (size_t)N * nx * nx;             // QCA_d, [d][ny][nx]
-    double *ABh = QCAh + (size_t)N * ny * nx;           // Ad^d Bd, [d][nx][nu]
+    // QCA_d = Q Cd Ad^(d+1) (for Fx = 2 (Sx' Qbar Su)', :307), by the recurrences AB_d = Ad AB_(d-1) and
+    // QCA_d = QCA_(d-1) Ad four horizon steps per barrier: with Ad^1..Ad^4 at hand, steps d0 .. d0+3 all
+    // come from step d0 - 1 (N / 4 barriers, and no Ad^k history: the LDS of two plants per CU).
+    double *QCAh = sm + S.QCAh;                         // QCA_d, [d][ny][nx]
+    double *ABh = sm + S.ABh;                           // Ad^d Bd, [d][nx][nu]
+    double *Pw = sm + S.Pw4;                            // Ad^(s+1) at Pw + s nx^2, s = 0..3
     double *QC = CA;                                    // Q Cd (ny x nx)
-    for (int e = t; e < nx * nx; e += T) Pw[e] = Ad[e];
-    for (int e = t; e < ny * nx; e += T) QC[e] = dot12(Q + (e / nx) * ny, 1, Cd + e % nx, nx, ny);
-    for (int e = t; e < nx * nu; e += T) ABh[e] = Bd[e];
+    const int ann = nx * nx, anu = nx * nu, ayx = ny * nx;
+    for (int e = t; e < ann; e += T) Pw[e] = Ad[e];
+    for (int e = t; e < ayx; e += T) QC[e] = dot12(Q + (e / nx) * ny, 1, Cd + e % nx, nx, ny);
+    for (int e = t; e < anu; e += T) ABh[e] = Bd[e];
     __syncthreads();
-    for (int have = 1; have < N; have *= 2) {  // Ad^k = Ad^have Ad^(k - have), have < k <= 2 have
-        const int fresh = (2 * have < N ? 2 * have : N) - have;
-        for (int it = t; it < fresh * nx * nx; it += T) {
-            const int kk = have + 1 + it / (nx * nx), i = (it / nx) % nx, j = it % nx;
-            Pw[(size_t)(kk - 1) * nx * nx + i * nx + j] =
-                dot12(Pw + (size_t)(have - 1) * nx * nx + i * nx, 1, Pw + (size_t)(kk - have - 1) * nx * nx + j, nx, nx);
+    for (int e = t; e < ann; e += T) Pw[ann + e] = dot12(Ad + (e / nx) * nx, 1, Ad + e % nx, nx, nx);  // Ad^2
+    for (int e = t; e < ayx; e += T) QCAh[e] = dot12(QC + (e / nx) * nx, 1, Ad + e % nx, nx, nx);     // QCA_0
+    __syncthreads();
+    for (int e = t; e < 2 * ann; e += T) {  // Ad^3 = Ad^2 Ad, Ad^4 = Ad^2 Ad^2
+        const int k = e / ann, f = e % ann;
+        Pw[(2 + k) * ann + f] = dot12(Pw + ann + (f / nx) * nx, 1, (k ? Pw + ann : Ad) + f % nx, nx, nx);
+    }
+    __syncthreads();
+    for (int d0 = 1; d0 < N; d0 += 4) {  // steps d0 .. d0 + 3 from step d0 - 1
+        const int steps = N - d0 < 4 ? N - d0 : 4;
+        for (int it = t; it < steps * (anu + ayx); it += T) {
+            const int sdx = it / (anu + ayx), e = it % (anu + ayx);
+            const double *Ps = Pw + sdx * ann;  // Ad^(sdx + 1)
+            if (e < anu) {  // AB_(d0 + sdx) = Ad^(sdx+1) AB_(d0 - 1)
+                const int i = e / nu, c = e % nu;
+                ABh[(size_t)(d0 + sdx) * anu + e] = dot12(Ps + i * nx, 1, ABh + (size_t)(d0 - 1) * anu + c, nu, nx);
+            } else {        // QCA_(d0 + sdx) = QCA_(d0 - 1) Ad^(sdx+1)
+                const int f = e - anu, i = f / nx, c = f % nx;
+                QCAh[(size_t)(d0 + sdx) * ayx + f] = dot12(QCAh + (size_t)(d0 - 1) * ayx + i * nx, 1, Ps + c, nx, nx);
+            }
         }
         __syncthreads();
     }
-    {
-        const int n1 = (N - 1) * nx * nu, n2 = N * ny * nx;
-        for (int it = t; it < n1 + n2; it += T) {
-            if (it < n1) {  // Ad^d Bd, d >= 1
-                const int d = 1 + it / (nx * nu), i = (it / nu) % nx, c = it % nu;
-                ABh[(size_t)d * nx * nu + i * nu + c] = dot12(Pw + (size_t)(d - 1) * nx * nx + i * nx, 1, Bd + c, nu, nx);
-            } else {  // QCA_d = (Q Cd) Ad^(d+1)
-                const int e = it - n1, d = e / (ny * nx), i = (e / nx) % ny, c = e % nx;
-                QCAh[e] = dot12(QC + i * nx, 1, Pw + (size_t)d * nx * nx + c, nx, nx);
-            }
-        }
-    }
-    __syncthreads();
     for (int it = t; it < N * ny * nu; it += T) {  // Cd Ad^d Bd
         const int d = it / (ny * nu), i = (it / nu) % ny, c = it % nu;
         CS[it] = dot12(Cd + i * nx, 1, ABh + (size_t)d * nx * nu + c, nu, nx);
@@ -215,11 +232,11 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
     // Fx_j = 2 sum_{d >= j} CS_{d-j}' QCA_d (block row j, nu x nx) on the matrix cores: Fx = sum_d A_d B_d
     // with A_d((j,r), kk) = CS_{d-j}(kk, r) (j <= d) and B_d = QCA_d, every horizon step accumulated in
     // the same 16 x 16 output tile (rows (j, r), columns c < nx <= 16); two waves per row tile split the
-    // steps by parity and add through LDS.  QCS_d = Q CS_d.
+    // steps by parity and add through LDS.  (Q CS_d is formed where it is read, below: no LDS copy.)
     {
         typedef double v4d __attribute__((ext_vector_type(4)));
         const int lane = t & 63, wv = t >> 6, nt = (n + 15) >> 4, nks = (ny + 3) >> 2;
-        double *part = P + S.hist;  // [tile][64 lanes][4], past the live histories
+        double *part = sm + S.part;  // [tile][64 lanes][4], past the live histories
         const int ti = wv % 8, half = wv / 8;
         v4d acc = {0.0, 0.0, 0.0, 0.0};
         if (ti < nt) {
@@ -246,10 +263,6 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
             }
         }
     }
-    for (int e = t; e < N * ny * nu; e += T) {
-        const int d = e / (ny * nu), i = (e / nu) % ny, c = e % nu;
-        QCS[e] = dot12(Q + i * ny, 1, CS + (size_t)d * ny * nu + c, nu, ny);
-    }
     __syncthreads();  // (the QCA history is dead: P is written below)
     MPCQ_SSTAMP(3);
 
@@ -274,50 +287,53 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
             for (int ks = 0; ks < nks; ks++) {
                 const int kk = ks * 4 + (lane >> 4);
                 const double av = (ga < n && kk < ny) ? CS[((size_t)ia * ny + kk) * nu + ra] : 0.0;
-                const double bv = (gb < n && kk < ny) ? QCS[((size_t)kb * ny + kk) * nu + cb] : 0.0;
+                const double bv = (gb < n && kk < ny) ? dot12(Q + kk * ny, 1, CS + (size_t)kb * ny * nu + cb, nu, ny) : 0.0;
                 acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
             }
 #pragma unroll
             for (int v = 0; v < 4; v++) {  // D(row = (lane >> 4) + 4 v, col = lane & 15)
                 const int gi = ti * 16 + (lane >> 4) + 4 * v, gk = gb;
                 const int i = gi / nu, r = gi % nu, k = kb, c = cb;
-                if (gi < n && gk < n && i >= k)
-                    P[(size_t)((N - 1 - i) * nu + r) * ldp + (N - 1 - k) * nu + c] = acc[v];
+                if (gi < n && gk < n && i >= k) {  // block (N-1-i, N-1-k): strictly upper, or a diagonal block
+                    if (i > k) P[pk_up((N - 1 - i) * nu + r, (N - 1 - k) * nu + c, n)] = acc[v];
+                    else Dblk[((N - 1 - i) * nu + r) * nu + c] = acc[v];
+                }
             }
         }
     }
     __syncthreads();
     // Fu = 2 (R' + H(j, 0)) per block (:305, the .diagonal() quirk as blocks; Q symmetric): block j of
     // sum_u CS_u' Q CS_(u+j) is G(j, N-1-j)', the last value of the scan over delta = j below
+    // P = (H1 + H1') / 2: an off-diagonal block's entry and its mirror come from the same scan, so the
+    // thread stores their mean; a diagonal block's (r, c) and (c, r) come from two scans (Dblk, merged below)
     for (int it = t; it < N * nu * nu; it += T) {
         const int dl = it / (nu * nu), r = (it / nu) % nu, c = it % nu;
         double acc = 0.0;
         for (int tt = 0; tt + dl < N; tt++) {
             const int j2 = N - 1 - tt, j1 = j2 - dl;
-            double *pe = P + (size_t)(j1 * nu + r) * ldp + j2 * nu + c;
+            double *pe = dl ? P + pk_up(j1 * nu + r, j2 * nu + c, n) : Dblk + (j1 * nu + r) * nu + c;
             acc += *pe;
             const double rr = (double)(N - j2);  // N - max(j1, j2)
-            *pe = 2.0 * (rr * R[r * nu + c] + (dl == 0 ? RD[r * nu + c] : 0.0) + acc);
-            if (dl > 0)  // H(j2, j1) = H(j1, j2)'
-                P[(size_t)(j2 * nu + c) * ldp + j1 * nu + r] = 2.0 * (rr * R[c * nu + r] + acc);
+            const double up = 2.0 * (rr * R[r * nu + c] + (dl == 0 ? RD[r * nu + c] : 0.0) + acc);
+            if (dl > 0) *pe = (up + 2.0 * (rr * R[c * nu + r] + acc)) / 2.0;  // H(j2, j1) = H(j1, j2)'
+            else *pe = up;
         }
         out[L.Fu + (dl * nu + c) * nu + r] = 2.0 * (R[r * nu + c] + acc);
     }
-    // Frs = -2 sum_{d <= N-1-j} QCS_d' (Fr = -2 (Qbar Su)', :306, summed over the horizon blocks)
+    // Frs = -2 sum_{d <= N-1-j} (Q CS_d)' (Fr = -2 (Qbar Su)', :306, summed over the horizon blocks)
     for (int it = t; it < n * ny; it += T) {
         const int j = it / (nu * ny), r = (it / ny) % nu, i = it % ny;
         double acc = 0.0;
-        for (int d = 0; d <= N - 1 - j; d++) acc += QCS[(size_t)d * ny * nu + i * nu + r];
+        for (int d = 0; d <= N - 1 - j; d++) acc += dot12(Q + i * ny, 1, CS + (size_t)d * ny * nu + r, nu, ny);
         out[L.Frs + it] = -2.0 * acc;
     }
     __syncthreads();
     MPCQ_SSTAMP(4);
-    for (int e = t; e < n * n; e += T) {
-        const int i = e / n, j = e % n;
-        if (i < j) {
-            const double v = (P[(size_t)i * ldp + j] + P[(size_t)j * ldp + i]) / 2.0;
-            P[(size_t)i * ldp + j] = v;
-            P[(size_t)j * ldp + i] = v;
+    for (int e = t; e < N * nu * nu; e += T) {  // the diagonal blocks into the packed triangle
+        const int j = e / (nu * nu), r = (e / nu) % nu, c = e % nu;
+        if (r <= c) {
+            const double v = Dblk[(j * nu + r) * nu + c];
+            P[pk_up(j * nu + r, j * nu + c, n)] = r == c ? v : (v + Dblk[(j * nu + c) * nu + r]) / 2.0;
         }
     }
     for (int j = t; j < n; j += T) { Dv[j] = 1.0; Ev[j] = 1.0; }
@@ -337,8 +353,8 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
 #pragma unroll
             for (int ii = 0; ii < 16; ii += 2) {
                 const int i = i0 + ii;
-                if (i < n) m0 = fmax(m0, Dv[i] * fabs(P[(size_t)i * ldp + cj]));
-                if (i + 1 < n) m1 = fmax(m1, Dv[i + 1] * fabs(P[(size_t)(i + 1) * ldp + cj]));
+                if (i < n) m0 = fmax(m0, Dv[i] * fabs(P[pk(i, cj, n)]));
+                if (i + 1 < n) m1 = fmax(m1, Dv[i + 1] * fabs(P[pk(i + 1, cj, n)]));
             }
             cm[sc * 128 + cj] = fmax(m0, m1);
         }
@@ -417,7 +433,7 @@ __global__ __launch_bounds__(kMimoSetupThreads) void mimo_setup_kernel(MimoSetup
     // ---- outputs: P^ = c D P D, D, E, c, SW (suffix sums of K0' diag(2 E_k^2) K0), row-type check
     for (int e = t; e < n * L.ldp; e += T) {
         const int i = e / L.ldp, j = e % L.ldp;
-        const double v = j < n ? ((cst * Dv[i]) * P[(size_t)i * ldp + j]) * Dv[j] : 0.0;
+        const double v = j < n ? ((cst * Dv[i]) * P[pk(i, j, n)]) * Dv[j] : 0.0;
         out[L.Ph + e] = v;
         // osqp_setup fails on a non-convex P (the reference's ctor: solverFlag false); a diagonal of
         // P^ + sigma I that is not positive proves it.  (Necessary only: a P with positive diagonal

@@ -19,58 +19,116 @@
 // into one m x (nx + 3) map once per operator set (mpcq_api.cpp build_order_map), and the key costs
 // m (nx + 2) fp64 FMAs per QP here.
 //
-// One thread per QP.  Bins: two per octave of |v| (OrderBins::bin), a counting scatter into fixed-capacity
-// per-bin lists (each bin can hold the whole batch: no global prefix, so one launch); the tile kernel's
-// phase 0 reads the 64 bin counts, forms their prefix in its prologue and maps its wave slots through it.
+// A counting sort in two launches: order_key_kernel bins the keys (OrderBins::bin: 16 bins per octave of
+// |v|) and takes each QP's rank inside its bin from a per-workgroup LDS histogram (256 QPs) and one
+// global atomic per (workgroup, bin); order_scatter_kernel (one thread per QP) forms the prefix of the bin
+// counts in every workgroup and writes list[prefix[bin] + rank] = QP.  The tile kernel's phase 0 reads its QPs
+// from the list and its workgroup 0 clears the counts for the next solve (AdmmArgs::ord_list, ord_zero).
 #include "mpcq_internal.h"
 
 namespace mpcq {
 
-__global__ __launch_bounds__(256) void order_bin_kernel(int batch, int nx, int m, const double *__restrict__ X,
-                                                        const double *__restrict__ U, const double *__restrict__ kmap,
-                                                        double xref, int *__restrict__ cnt, int *__restrict__ bins,
-                                                        int cap)
+// Four threads per QP (each a quarter of the m rows, fully unrolled so the map's LDS reads and the FMA chains
+// of different rows overlap), 256 QPs per 1,024-thread workgroup: the key's latency is spread over 16 waves
+// per workgroup, and a workgroup's global atomics (one per non-empty bin) cover 256 QPs.
+constexpr int kOrderThreads = 1024, kOrderQPW = kOrderThreads / 4;
+__global__ __launch_bounds__(kOrderThreads) void order_key_kernel(int batch, int nx, int m, const double *__restrict__ X,
+                                                                  const double *__restrict__ U,
+                                                                  const double *__restrict__ kmap, double xref,
+                                                                  int *__restrict__ cnt, int *__restrict__ key)
 {
-    constexpr int KB = OrderBins::kBins, KS = OrderBins::kStride;
+    constexpr int KB = OrderBins::kBins, KS = OrderBins::kStride, RPT = OrderBins::kMaxRows / 4;
     __shared__ double k[OrderBins::kMaxRows * KS];
     __shared__ int h[KB], base[KB];
-    for (int i = threadIdx.x; i < m * KS; i += blockDim.x) k[i] = kmap[i];
-    if (threadIdx.x < KB) h[threadIdx.x] = 0;
-    __syncthreads();
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    int bin = 0, loc = 0;
-    if (b < batch) {
-        double x[8];
+    for (int i = threadIdx.x; i < m * KS; i += blockDim.x) k[i] = i % KS == 9 ? __builtin_fma(kmap[i + 1], xref, kmap[i]) : kmap[i];
+    for (int i = threadIdx.x; i < KB; i += blockDim.x) h[i] = 0;
+    const int part = threadIdx.x & 3;
+    const int b = blockIdx.x * kOrderQPW + (threadIdx.x >> 2);
+    const int bb = b < batch ? b : batch - 1;
+    double x[8];
 #pragma unroll
-        for (int t = 0; t < 8; t++) x[t] = t < nx ? X[(size_t)b * nx + t] : 0.0;
-        const double u = U[b];
-        double v = -__builtin_inf();
-        for (int j = 0; j < m; j++) {
+    for (int t = 0; t < 8; t++) x[t] = t < nx ? X[(size_t)bb * nx + t] : 0.0;
+    const double u = U[bb];
+    __syncthreads();
+    // rows part, part + 4, ... (interleaved: the four threads of a QP read different rows of one LDS line)
+    double v = -__builtin_inf();
+#pragma unroll
+    for (int q = 0; q < RPT; q++) {
+        const int j = 4 * q + part;
+        if (j < m) {
             const double *r = k + KS * j;
-            double s = __builtin_fma(r[10], xref, r[9]);  // (-A P^-1 Fr 1) xref - W0
+            double s = r[9];  // (-A P^-1 Fr 1) xref - W0, formed above
 #pragma unroll
             for (int t = 0; t < 8; t++)
                 if (t < nx) s = __builtin_fma(r[t], x[t], s);
             s = __builtin_fma(r[8], u, s);
             v = __builtin_fmax(v, s);
         }
+    }
+    v = __builtin_fmax(v, __shfl_xor(v, 1));  // the QP's four quarters (lanes 4 i .. 4 i + 3)
+    v = __builtin_fmax(v, __shfl_xor(v, 2));
+    int bin = 0, loc = 0;
+    if (part == 0 && b < batch) {
         bin = OrderBins::bin(v);
         loc = atomicAdd(&h[bin], 1);
     }
     __syncthreads();
-    if (threadIdx.x < KB && h[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cnt[threadIdx.x], h[threadIdx.x]);
+    for (int i = threadIdx.x; i < KB; i += blockDim.x)
+        if (h[i]) base[i] = atomicAdd(&cnt[i], h[i]);
     __syncthreads();
-    if (b < batch) bins[(size_t)bin * cap + base[bin] + loc] = b;
+    if (part == 0 && b < batch) key[b] = (bin << OrderBins::kRankBits) | (base[bin] + loc);
+}
+
+__global__ __launch_bounds__(256) void order_scatter_kernel(int batch, const int *__restrict__ cnt,
+                                                            const int *__restrict__ key, int *__restrict__ list)
+{
+    constexpr int KB = OrderBins::kBins, PER = KB / 256;
+    static_assert(KB % 256 == 0, "bins per thread");
+    __shared__ int pre[KB], wsum[4];
+    // exclusive prefix of the bin counts: PER consecutive bins per thread, then a 256-thread scan
+    int loc[PER], tot = 0;
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+        loc[i] = tot;
+        tot += cnt[threadIdx.x * PER + i];
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int inc = tot;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(inc, d);
+        if (lane >= d) inc += t;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    int off = inc - tot;
+    for (int i = 0; i < w; i++) off += wsum[i];
+#pragma unroll
+    for (int i = 0; i < PER; i++) pre[threadIdx.x * PER + i] = off + loc[i];
+    __syncthreads();
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < batch) {
+        const int kv = key[b];
+        const int pos = pre[kv >> OrderBins::kRankBits] + (kv & ((1 << OrderBins::kRankBits) - 1));
+        if (pos < batch) list[pos] = b;  // (always: the counts sum to batch)
+    }
 }
 
 }  // namespace mpcq
 
-// cnt: OrderBins::kBins counters, zero on entry (the caller clears them on the stream first).
-extern "C" int mpcq_internal_order_bins(int batch, int nx, int m, const double *X, const double *U, const double *kmap,
-                                        double xref, int *cnt, int *bins, int cap, hipStream_t s)
+// cnt: OrderBins::kBins counters, zero on entry (cleared by the previous ordered tile launch, or by the
+// caller); key: batch ints of scratch; list: batch ints, the QPs hardest first.
+extern "C" int mpcq_internal_order(int batch, int nx, int m, const double *X, const double *U, const double *kmap,
+                                   double xref, int *cnt, int *key, int *list, hipStream_t s)
 {
-    if (batch <= 0 || nx <= 0 || nx > 8 || m <= 0 || m > mpcq::OrderBins::kMaxRows || cap < batch) return -1;
-    hipLaunchKernelGGL(mpcq::order_bin_kernel, dim3((batch + 255) / 256), dim3(256), 0, s, batch, nx, m, X, U, kmap,
-                       xref, cnt, bins, cap);
+    if (batch <= 0 || batch >= (1 << mpcq::OrderBins::kRankBits) || nx <= 0 || nx > 8 || m <= 0 ||
+        m > mpcq::OrderBins::kMaxRows)
+        return -1;
+    const int blocks = (batch + 255) / 256;
+    hipLaunchKernelGGL(mpcq::order_key_kernel, dim3((batch + mpcq::kOrderQPW - 1) / mpcq::kOrderQPW),
+                       dim3(mpcq::kOrderThreads), 0, s, batch, nx, m, X, U, kmap, xref, cnt, key);
+    if (hipGetLastError() != hipSuccess) return -2;
+    hipLaunchKernelGGL(mpcq::order_scatter_kernel, dim3(blocks), dim3(256), 0, s, batch, (const int *)cnt,
+                       (const int *)key, list);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }

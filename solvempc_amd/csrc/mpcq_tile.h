@@ -426,22 +426,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
         if (a.zero_cnt) a.zero_cnt[threadIdx.x * ListSeg::kStride] = 0;
         if (a.zero_cnt0) a.zero_cnt0[threadIdx.x * ListSeg::kStride] = 0;
     }
+    if (blockIdx.x == 0 && a.ord_zero)  // the order's bin counters, read by its finished sort: the next solve's
+        for (int i = threadIdx.x; i < OrderBins::kBins; i += NTH) a.ord_zero[i] = 0;
     if (blk * (refill ? WPB * a.sim.cpw : QPW) >= count) return;  // whole workgroup idle in this phase (uniform)
-    // phase 0 in hardest-first order (mpcq_order.hip): the prefix of the 64 bin counts, s_pref[k] = the
-    // first slot of bin k (one wave scans; read after the barrier below)
-    __shared__ int s_pref[OrderBins::kBins + 1];
-    const bool ordered = a.ord_cnt != nullptr && !seglist && !refill;
-    static_assert(OrderBins::kBins == 64, "one bin per lane of the scanning wave");
-    if (ordered && threadIdx.x < 64) {
-        int v = a.ord_cnt[threadIdx.x];
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int t = __shfl_up(v, d);
-            if ((int)threadIdx.x >= d) v += t;
-        }
-        s_pref[threadIdx.x + 1] = v;
-        if (threadIdx.x == 0) s_pref[0] = 0;
-    }
+    const bool ordered = a.ord_list != nullptr && !seglist && !refill;  // phase 0 hardest-first (mpcq_order.hip)
     for (int i = threadIdx.x; i < NCP; i += NTH) {
         s_lam[i] = a.ops.lam[i];
         s_D[i] = a.ops.D[i];
@@ -1857,13 +1845,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             int qp = a.qp0 + i;
             if (seglist) {
                 qp = a.list_in[i];
-            } else if (ordered) {  // slot -> bin k (s_pref[k] <= slot < s_pref[k + 1]) -> that bin's list
-                int k = 0;
-#pragma unroll
-                for (int st = 32; st; st >>= 1)
-                    if (s_pref[k + st] <= slot) k += st;
-                qp = a.ord_bins[(size_t)k * a.ord_cap + (slot - s_pref[k])];
-                qp = qp < 0 ? 0 : (qp >= a.batch ? a.batch - 1 : qp);  // (the lists hold batch indices only)
+            } else if (ordered && valid[gi]) {
+                qp = a.ord_list[i];
+                qp = qp < 0 ? 0 : (qp >= a.batch ? a.batch - 1 : qp);  // (the list holds batch indices only)
             }
             b_[gi] = valid[gi] ? qp : 0;
         }
@@ -1933,6 +1917,59 @@ int tile_launch(const AdmmArgs<T> &a, hipStream_t s)
     return tile_launch_variant<T, KN, KM, false, false, 1, 2>(a, s);
 }
 
+// Lazily published solution of a tile solve (osqp store_solution, read by getSolution :105 only when a
+// caller asks: mpcq_api.cpp materialize_xy).  The tile finalize stores the warm state x' (W-basis), z, y,
+// rho, status and U += x(0); x = D W x' and y = E y / c are formed here, for every QP, with the finalize's
+// own arithmetic (the same MFMA product of the same W image, the same roundings): bit for bit what an eager
+// finalize would have written.  One 16-QP column group per wave, index order.
+template <typename T, int KN, int KM, bool PAIRED>
+__global__ __launch_bounds__(256) void tile_publish_kernel(AdmmArgs<T> a)
+{
+    constexpr int VEC = 16 / sizeof(T);
+    constexpr TileLayout L = TileLayout::make(KN, KM, VEC, PAIRED);
+    constexpr size_t IMG0 = PAIRED ? TileLayout::make(KN, KM, VEC, false).total : 0;
+    constexpr int NT = L.NT, MT = L.MT, KNP = L.KNP;
+    constexpr int NS = 4 * NT, MS = 4 * MT, NCP = 16 * NT, MCP = 16 * MT;
+    const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+    const int w = (int)blockIdx.x * 4 + ((int)threadIdx.x >> 6);
+    if (16 * w >= a.batch) return;  // (wave-uniform)
+    const int b = 16 * w + c;
+    const bool valid = b < a.batch;
+    const int bb = valid ? b : a.batch - 1;
+    const int n = a.n, m = a.m;
+    T xs[1][NS], xh[1][NS];
+#pragma unroll
+    for (int s = 0; s < NS; s++) xs[0][s] = s < KN ? a.xs[(size_t)bb * NCP + 4 * s + g] : T(0);
+    tile_mv_g<T, 1, NT, KN, KNP>(a.img + IMG0 + L.W, xs, xh, lane, nullptr);
+    if (!valid) return;
+    const int sta = a.status[b];
+    const bool has_sol = sta == kSolved || sta == kSolvedInaccurate || sta == kMaxIterReached;
+    const double cinv64 = (double)a.ops.cs[1];
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        const int v = 4 * s + g;
+        if (s < KN && v < n) a.x[(size_t)b * n + v] = has_sol ? (double)xh[0][s] * (double)a.ops.D[v] : __builtin_nan("");
+    }
+#pragma unroll
+    for (int s = 0; s < MS; s++) {
+        const int v = 4 * s + g;
+        if (s < KM && v < m)
+            a.y[(size_t)b * m + v] = has_sol ? ((double)a.ys[(size_t)b * MCP + 4 * s + g] * (double)a.ops.E[v]) * cinv64
+                                             : __builtin_nan("");
+    }
+}
+
+template <typename T, int KN, int KM>
+int tile_publish(const AdmmArgs<T> &a, bool paired, hipStream_t s)
+{
+    const int waves = (a.batch + 15) / 16;
+    if (paired && KM == 2 * KN)
+        hipLaunchKernelGGL((tile_publish_kernel<T, KN, KM, KM == 2 * KN>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((tile_publish_kernel<T, KN, KM, false>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 // Compiled (KN, KM) = (ceil(n/4), ceil(m/4)): the reference horizons N = 15 (n 15, m 30) and N = 20
 // (n 20, m 40), plus two small shapes for the generic-QP tests.
 #define MPCQ_TILE_SHAPES(X) X(1, 1) X(2, 3) X(4, 8) X(5, 10)
@@ -1941,6 +1978,15 @@ template <typename T>
 int tile_launch_any(const AdmmArgs<T> &a, int KN, int KM, hipStream_t s)
 {
 #define MPCQ_TRY(KN_, KM_) if (KN == KN_ && KM == KM_) return tile_launch<T, KN_, KM_>(a, s);
+    MPCQ_TILE_SHAPES(MPCQ_TRY)
+#undef MPCQ_TRY
+    return -1;
+}
+
+template <typename T>
+int tile_publish_any(const AdmmArgs<T> &a, int KN, int KM, bool paired, hipStream_t s)
+{
+#define MPCQ_TRY(KN_, KM_) if (KN == KN_ && KM == KM_) return tile_publish<T, KN_, KM_>(a, paired, s);
     MPCQ_TILE_SHAPES(MPCQ_TRY)
 #undef MPCQ_TRY
     return -1;

@@ -10,3 +10,8 @@ extern "C" int mpcq_internal_tile_stream_launch_f32(const mpcq::AdmmArgs<float> 
 {
     return mpcq::tile_stream_launch_any<float>(*a, KN, KM, s);
 }
+
+extern "C" int mpcq_internal_tile_publish_f32(const mpcq::AdmmArgs<float> *a, int KN, int KM, int paired, hipStream_t s)
+{
+    return mpcq::tile_publish_any<float>(*a, KN, KM, paired != 0, s);
+}

@@ -10,3 +10,8 @@ extern "C" int mpcq_internal_tile_stream_launch_f64(const mpcq::AdmmArgs<double>
 {
     return mpcq::tile_stream_launch_any<double>(*a, KN, KM, s);
 }
+
+extern "C" int mpcq_internal_tile_publish_f64(const mpcq::AdmmArgs<double> *a, int KN, int KM, int paired, hipStream_t s)
+{
+    return mpcq::tile_publish_any<double>(*a, KN, KM, paired != 0, s);
+}

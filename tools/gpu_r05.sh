@@ -17,15 +17,29 @@ for step in "$@"; do
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 \
         || { echo "smoke failed"; tail -20 "$out/smoke.log"; exit 1; } ;;
-    bench)
-      timeout -k 10 600 python -u bench.py $arg > "$out/bench_${arg// /_}.json" 2> "$out/bench_${arg// /_}.err" \
-        || { echo "bench failed"; tail -20 "$out/bench_${arg// /_}.err"; exit 1; } ;;
+    bench)  # bench:<args with _ for spaces>, e.g. bench:--workload_quadrotor
+      timeout -k 10 600 python -u bench.py ${arg//_/ } > "$out/bench_$arg.json" 2> "$out/bench_$arg.err" \
+        || { echo "bench failed"; tail -20 "$out/bench_$arg.err"; exit 1; } ;;
     probe)
       timeout -k 10 600 python -u tools/order_probe.py $arg > "$out/probe_$arg.log" 2>&1 \
         || { echo "probe failed"; tail -20 "$out/probe_$arg.log"; exit 1; } ;;
     prof)
       (cd "$out" && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d prof -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 3 --variants 0 --cpu-seconds 0 $arg \
         > prof.log 2>&1) || { echo "prof failed"; tail -20 "$out/prof.log"; exit 1; } ;;
+    pmc)  # pmc:<workload>,<dtype>[,<extra PMC set>] -> $out/pmc_<workload>_<dtype>/ (FETCH, WRITE, MFMA/VALU passes)
+      IFS=, read -r wl dt extra <<< "$arg"
+      sets=$'FETCH_SIZE\nWRITE_SIZE\nSQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE'
+      [ -n "$extra" ] && sets="$sets"$'\n'"${extra//+/ }"
+      CMD="python bench.py --workload $wl --dtype $dt --steps 3 --warmup 1 --cpu-seconds 0 --variants 0" \
+        PMC_SETS="$sets" timeout -k 10 600 bash tools/pmc.sh "$dt" "$out/pmc_${wl}_$dt" > "$out/pmc_${wl}_$dt.log" 2>&1 \
+        || { echo "pmc failed"; cat "$out/pmc_${wl}_$dt/passes.txt"; exit 1; } ;;
+    stamps)  # stamps:mimo_setup -> per-stage cycles of mimo_setup_kernel on the debug library built here
+             # beforehand (SRC=mpcq_mimo.hip DBGDIR=tools/dbg_r05 bash tools/build_dbg.sh)
+      MPCQ_LIBRARY=tools/dbg_r05/libmpcq.so timeout -k 10 300 python -u tools/mimo_setup_stamps.py > "$out/stamps_$arg.log" 2>&1 \
+        || { echo "stamps failed"; tail "$out/stamps_$arg.log"; exit 1; } ;;
+    calib)  # WRITE_SIZE calibration of the finalize's store patterns (tools/calib/write_calib.hip, built here)
+      (cd "$out" && timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d calib -o run -- "$GRAFT_REPO_ROOT/tools/calib/write_calib" \
+        > calib.log 2>&1) || { echo "calib failed"; tail "$out/calib.log"; exit 1; } ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   echo "step $step ok"
