@@ -47,10 +47,13 @@ constexpr int kMaxPhases = 16;
 //   MPCQ_STREAM=graph|wave      mpcq_mpc_run_device's per-step graph or one-QP-per-wave launch
 //                               (mpcq_get_stream_path reports the choice)
 //   MPCQ_STREAM_CPW=k           plants per wave of the tile stream mode
+//   MPCQ_STREAM_OCC=1           the tile stream mode's one-wave-per-SIMD variant (when the waves fit)
 //   MPCQ_TAIL=wave|tile         the tile chain's last launch on the one-QP-per-wave / tile kernel
 //   MPCQ_MIX_R=r                MPCQ_F64_MIXED: fp64 iterations per check interval (default MPCQ_MIX_R)
 //   MPCQ_TILE_OCC=2|3           waves per SIMD of the f32 paired tile kernel (default 3)
 //   MPCQ_PLANT_WPE=2|3|4        waves per SIMD of the one-pass per-plant kernel (default f64 3, f32 2)
+//   MPCQ_ORDER=0                a shared-plant MPC step's tile solve in index order (default: hardest first)
+//   MPCQ_LAZY_XY=0              the tile solve stores x, y at finalize (default: published on demand)
 // Debug builds (-DMPCQ_DEBUG_HOOKS) add the stamp / profiling dumps (MPCQ_TILE_STAMPS,
 // MPCQ_SETUP_PROF, MPCQ_MIMO_SETUP_STAMPS, MPCQ_MIMO_STAMPS) and MPCQ_DEBUG_SYNC.
 const char *test_hook(const char *name)
@@ -149,12 +152,17 @@ struct mpcq_ctx {
     // materialize_xy before anything reads them (get_solution / get_dual, the device view, verbose, or a
     // call that overwrites the warm state)
     bool xy_lazy = false;
+    // the same solve's rho (fp64 contexts): its warm-state rho d_rhos is the reported one; d_rho is copied
+    // from it by materialize_rho before anything reads d_rho (get_info, the device view, verbose) or a
+    // reset overwrites d_rhos
+    bool rho_lazy = false;
     // host copies of plant-0 scaling
     std::vector<double> hD, hE;
     double hc = 1.0;
 };
 
 static int materialize_xy(mpcq_ctx *c);  // (below: the lazy x, y of a tile solve)
+static int materialize_rho(mpcq_ctx *c);  // (and its rho)
 
 namespace {
 
@@ -212,6 +220,10 @@ mpcq::AdmmArgs<T> make_args(mpcq_ctx *c)
     a.ops_stride = c->ops_stride;
     a.ctype = c->d_ctype;
     a.st = to_solver(c->set);
+    a.eps10[0] = (T)a.st.eps_abs * T(10);
+    a.eps10[1] = (T)a.st.eps_rel * T(10);
+    a.eps10[2] = (T)a.st.eps_prim_inf * T(10);
+    a.eps10[3] = (T)a.st.eps_dual_inf * T(10);
     const int ct = c->set.check_termination;
     a.adaptive_interval = c->set.adaptive_rho_interval ? c->set.adaptive_rho_interval : (ct ? 4 * ct : 100);
     a.all_ineq = c->all_ineq;
@@ -250,6 +262,7 @@ mpcq::AdmmArgs<T> make_args(mpcq_ctx *c)
 int reset_state(mpcq_ctx *c, bool reset_rho)
 {
     if (int rc = materialize_xy(c)) return rc;  // (the warm state it zeroes is the last solve's x, y)
+    if (int rc = materialize_rho(c)) return rc;
     const size_t B = c->dims.batch, es = c->dims.dtype == MPCQ_F32 ? 4 : 8;
     HIPCHK(hipMemsetAsync(c->d_xs, 0, es * c->nc * B, c->last));
     HIPCHK(hipMemsetAsync(c->d_zs, 0, es * c->mc * B, c->last));
@@ -813,9 +826,12 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
         // the counters are zero unless the last ordered sort's tile launch did not run (it clears them)
         if (!c->ord_clean && hipMemsetAsync(ord_cnt, 0, 4 * (size_t)mpcq::OrderBins::kBins, s) != hipSuccess) return -2;
         c->ord_clean = false;
-        if (mpcq_internal_order(B, c->nx, c->dims.m, a.X, a.U, c->d_ordmap, a.xref, ord_cnt, ord_key, ord_list, s) != 0)
+        if (mpcq_internal_order(B, c->nx, c->dims.m, a.X, a.U, c->d_ordmap, a.xref, ord_cnt, ord_key, ord_list,
+                                a.X_save, a.U_save, s) != 0)
             return -2;
     }
+    // (an ordered step's X, U copies are the order kernel's: its phase-0 tile launch skips them)
+    double *const X_save = a.X_save, *const U_save = a.U_save;
     const int seg = mpcq::ListSeg::cap(B);
     const size_t lcap = (size_t)mpcq::ListSeg::kShards * seg;
     // Counter blocks: launch p zeroes block p + 1 (its successor's output) and a chain's final launch,
@@ -834,6 +850,8 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
     if (lazy_xy) {
         a.x = nullptr;
         a.y = nullptr;
+        // fp64 state: the finalize stores rho once, as warm state (materialize_rho reports it)
+        if (std::is_same<T, double>::value) a.rho_out = nullptr;
     }
 
     // debug build: per-wave stage stamps of every phase launch, written to $MPCQ_TILE_STAMPS after the solve
@@ -851,6 +869,8 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
         a.count_out = c->d_counts + (size_t)p * mpcq::ListSeg::kCounters;
         a.it_state = c->d_itstate;
         a.ord_list = (ordered && p == 0) ? ord_list : nullptr;
+        a.X_save = (ordered && p == 0) ? nullptr : X_save;
+        a.U_save = (ordered && p == 0) ? nullptr : U_save;
         a.ord_zero = (ordered && p == 0) ? ord_cnt : nullptr;
         a.stop_iter = stops[p];
         a.resume = p > 0;
@@ -886,6 +906,7 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
         np_run = p + 1;
     }
     c->xy_lazy = lazy_xy;
+    c->rho_lazy = lazy_xy && std::is_same<T, double>::value;
     if (stp && *stp) {
         std::vector<long long> h(8 * waves * kMaxPhases);
         if (hipMemcpyAsync(h.data(), c->d_stamps, 8 * h.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -1011,7 +1032,7 @@ static void verbose_solve(mpcq_ctx *c, double seconds)
     const size_t B = c->dims.batch, n = c->dims.n, m = c->dims.m;
     std::vector<int> st(B), it(B);
     std::vector<double> rho(B), x(n), y(m), q(n), u(m), l(m), P(n * n), A(m * n);
-    if (materialize_xy(c) != MPCQ_OK || hipStreamSynchronize(c->last) != hipSuccess ||
+    if (materialize_xy(c) != MPCQ_OK || materialize_rho(c) != MPCQ_OK || hipStreamSynchronize(c->last) != hipSuccess ||
         hipMemcpy(st.data(), c->d_status, 4 * B, hipMemcpyDeviceToHost) != hipSuccess ||
         hipMemcpy(it.data(), c->d_iter, 4 * B, hipMemcpyDeviceToHost) != hipSuccess ||
         hipMemcpy(rho.data(), c->d_rho, 8 * B, hipMemcpyDeviceToHost) != hipSuccess ||
@@ -1076,6 +1097,7 @@ static int launch_solve(mpcq_ctx *c, hipStream_t s, bool mpc, const double *X, d
     const auto t0 = std::chrono::steady_clock::now();
     c->ord_last = false;  // (launch_phases sets it for a hardest-first tile solve)
     c->xy_lazy = false;   // (and this, for a chain that publishes x, y lazily)
+    c->rho_lazy = false;  // (the solve below writes d_rho, or leaves it lazy again)
     const int rc = c->dims.dtype == MPCQ_F32 ? launch_typed<float>(c, s, mpc, X, U, xref)
                                              : launch_typed<double>(c, s, mpc, X, U, xref);
     if (rc) return fail(MPCQ_ERR_HIP, std::string("ADMM kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
@@ -1139,6 +1161,7 @@ int mpcq_get_info(mpcq_ctx *c, int *status, int *iter, double *rho)
     int rc = check_ctx(c, kAnySetup);
     if (rc) return rc;
     const size_t B = c->dims.batch;
+    if (rho && (rc = materialize_rho(c))) return rc;
     if ((rc = d2h(c, status, c->d_status, 4 * B))) return rc;
     if ((rc = d2h(c, iter, c->d_iter, 4 * B))) return rc;
     return d2h(c, rho, c->d_rho, 8 * B);
@@ -1190,7 +1213,7 @@ int mpcq_device_view_get(mpcq_ctx *c, mpcq_device_view *v)
 {
     if (!c || !v) return fail(MPCQ_ERR_ARG, "null argument");
     int rc = materialize_qu(c);  // (enqueued on the context's last stream)
-    if (rc || (rc = materialize_xy(c))) return rc;
+    if (rc || (rc = materialize_xy(c)) || (rc = materialize_rho(c))) return rc;
     v->q = c->d_q;
     v->u = c->d_u;
     v->l = c->d_l;
@@ -1250,6 +1273,15 @@ static int materialize_xy(mpcq_ctx *c)
         rc = mpcq_internal_tile_publish_f64(&a, c->KN, c->KM, a.paired = c->paired && c->all_ineq && c->lower_free, c->last);
     }
     return rc ? fail(MPCQ_ERR_HIP, "solution publish kernel failed") : MPCQ_OK;
+}
+
+// d_rho of the last tile solve from its warm-state rho (fp64: the same value), once.
+static int materialize_rho(mpcq_ctx *c)
+{
+    if (!c->rho_lazy) return MPCQ_OK;
+    c->rho_lazy = false;
+    HIPCHK(hipMemcpyAsync(c->d_rho, c->d_rhos, 8 * (size_t)c->dims.batch, hipMemcpyDeviceToDevice, c->last));
+    return MPCQ_OK;
 }
 
 // The bound-violation map of the hardest-first order (mpcq_order.hip) for a shared plant with MPC
@@ -1437,6 +1469,7 @@ template <typename T>
 static int launch_stream(mpcq_ctx *c, hipStream_t s, double *X, double *U, double xref, const mpcq::StreamArgs &sa)
 {
     c->xy_lazy = false;  // (the stream writes every QP's x, y at its last step)
+    c->rho_lazy = false;  // (and rho)
     auto a = make_args<T>(c);
     a.mpc = 1; a.mpc_u = 1; a.nx = c->nx; a.X = X; a.U = U; a.xref = xref;
     a.Fx = c->d_Fx; a.Fu = c->d_Fu; a.Fr = c->d_Fr; a.Sbar = c->d_Sbar; a.Ku = c->d_Ku; a.W0 = c->d_W0;
@@ -1460,6 +1493,7 @@ template <typename T>
 static int launch_tile_stream(mpcq_ctx *c, hipStream_t s, double *X, double *U, double xref, mpcq::StreamArgs sa)
 {
     c->xy_lazy = false;  // (the stream writes every QP's x, y at its last step)
+    c->rho_lazy = false;  // (and rho)
     const mpcq_settings &st = c->set;
     const int ct = st.check_termination;
     auto a = make_args<T>(c);
@@ -1470,6 +1504,12 @@ static int launch_tile_stream(mpcq_ctx *c, hipStream_t s, double *X, double *U, 
     // measured faster at half the SIMDs (config 5: cpw 4 103.7 M QP/s, 6-16 105.5-106.3 M, r04w_*)
     const long per = ((long)c->dims.batch + simds - 1) / simds * (c->dims.dtype == MPCQ_F32 ? 1 : 2);
     sa.cpw = *e ? std::max(1, std::min(16, std::atoi(e))) : (int)std::max<long>(1, std::min<long>(16, per));
+    // the kernel compiled for two waves per SIMD (its plant and check code spill outside the hot loop); the
+    // variant compiled for one (no spills, MFMA accumulators in AGPRs) measured 2 % slower at config 5
+    // (103.7 against 106.0 M QP/s, profiles/r05h_cfg5_occ_ab.jsonl): test hook MPCQ_STREAM_OCC=1 for A/B,
+    // taken only when the waves fit one per SIMD
+    const long waves = ((long)c->dims.batch + sa.cpw - 1) / sa.cpw;
+    sa.occ = (waves <= simds && test_hook("MPCQ_STREAM_OCC")[0] == '1') ? 1 : 2;
     a.mpc = 1; a.mpc_u = 1; a.nx = c->nx; a.X = X; a.U = U; a.xref = xref;
     a.Fx = c->d_Fx; a.Fu = c->d_Fu; a.Fr = c->d_Fr; a.Sbar = c->d_Sbar; a.Ku = c->d_Ku; a.W0 = c->d_W0;
     a.X_save = c->d_Xs; a.U_save = c->d_Us;  // the last step's X, U: its q, u on demand (materialize_qu)
@@ -1707,7 +1747,8 @@ int mpcq_mpc_plants_step_device(mpcq_ctx *c, int nx, int s_rows, const double *A
 {
     int rc = check_generic_dims(c);
     if (rc) return rc;
-    if ((rc = materialize_xy(c))) return rc;  // (a pending lazy x, y first: the kernel below rewrites the state)
+    if ((rc = materialize_xy(c)) || (rc = materialize_rho(c))) return rc;  // (a pending lazy x, y, rho first: the
+                                                                             // kernel below rewrites the state)
     const int n = c->dims.n, m = c->dims.m;
     if (nx <= 0 || nx > 8 || s_rows < 0) return fail(MPCQ_ERR_ARG, "plants_step: 1 <= nx <= 8, s_rows >= 0");
     if (m != 2 * n || n > 32) return fail(MPCQ_ERR_ARG, "plants_step: n = N <= 32, m = 2N (ModelPredictiveControlAPI.cpp:47-48)");

@@ -169,6 +169,8 @@ struct StreamArgs {
     unsigned long long seed;
     long long first_qp, first_step;
     double noise_std;
+    int occ;                      // tile stream: waves per SIMD the kernel is compiled for (1: at most one
+                                  // wave per SIMD, the whole register file, no spills; 2 otherwise)
 };
 
 template <typename T>
@@ -234,6 +236,9 @@ struct AdmmArgs {
     int mix_r;
     // waves per SIMD of the f32 paired tile kernel (0: the default, 3; 2: the OCC-2 variant)
     int tile_occ;
+    // (T) eps_abs, eps_rel, eps_prim_inf, eps_dual_inf times T(10), formed on the host in T: the tile
+    // kernel's approximate check_termination (OSQP auxil.c, the 10x tolerances after max_iter)
+    T eps10[4];
 };
 
 // MFMA operand images of one shared plant for the tile kernel (mpcq_tile.h).  A vector of length
@@ -428,9 +433,10 @@ int mpcq_internal_front_end(int batch, int nx, int n, int m, const double *Xs, c
                             const double *Ku, const double *W0, double *q, double *u, hipStream_t s);
 int mpcq_internal_set_step(long long *step, long long v, hipStream_t s);
 // Hardest-first order of a shared-plant MPC step (mpcq_order.hip): per-QP bound-violation key from the
-// host's OrderBins map, counting-sorted into list (cnt: OrderBins::kBins counters, zero on entry).
+// host's OrderBins map, counting-sorted into list (cnt: OrderBins::kBins counters, zero on entry); Xs, Us
+// (or null): copies of X, U for the step's q, u on demand.
 int mpcq_internal_order(int batch, int nx, int m, const double *X, const double *U, const double *kmap, double xref,
-                        int *cnt, int *key, int *list, hipStream_t s);
+                        int *cnt, int *key, int *list, double *Xs, double *Us, hipStream_t s);
 // MIMO condensed MPC (mpcq_mimo.hip): per-plant condensing + Ruiz + P^, then the per-QP solve
 // (one 512-thread workgroup per QP: KKT inverse by Gauss-Jordan in VGPRs, structured A).
 int mpcq_internal_mimo_setup_launch(const mpcq::MimoSetupArgs *a, hipStream_t s);

@@ -6,7 +6,9 @@
 // pipeline for 262,144 distinct MIMO plants per GPU; its formulation is oracle/mpc_mimo.h (every SISO
 // scalar a block).  Two kernels:
 //
-//  * mimo_setup_kernel — one 256-thread workgroup per plant, everything in LDS.  The horizon-stacked
+//  * mimo_setup_kernel — one 1024-thread workgroup (16 waves) per plant, two per CU, everything in LDS
+//    (under 80 KiB per plant at config 4: P as its packed upper triangle, regions shared by lifetime,
+//    MimoSetupShape).  The horizon-stacked
 //    contraction H = Su' Qbar Su is never formed densely: Su is block-Toeplitz (Su(i, j) = CS_{i-j},
 //    CS_d = sum_{k<=d} Cd Ad^k Bd), so H(j1, j1+delta) is a prefix sum over the horizon,
 //    G(delta, T) = sum_{t<=T} CS_{t+delta}' Q CS_t, and all of P costs N^2 nu^2 n_y multiply-adds
@@ -162,6 +164,11 @@ __global__ __launch_bounds__(kMimoSetupThreads, 8) void mimo_setup_kernel(MimoSe
         if (a.stamps && t == 0) a.stamps[(size_t)pl * 16 + (k)] = (long long)__builtin_amdgcn_s_memtime(); \
     } while (0)
     MPCQ_SSTAMP(0);
+    if (a.stamps && t == 0) {  // (debug: where and when the workgroup ran, for co-residency)
+        a.stamps[(size_t)pl * 16 + 12] = (long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+        a.stamps[(size_t)pl * 16 + 13] = (long long)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+        a.stamps[(size_t)pl * 16 + 14] = (long long)__builtin_amdgcn_s_memrealtime();
+    }
 
     // ---- plant data -> LDS
     for (int e = t; e < nx * nx; e += T) Ad[e] = a.Ad[(size_t)pl * nx * nx + e];
@@ -180,41 +187,48 @@ __global__ __launch_bounds__(kMimoSetupThreads, 8) void mimo_setup_kernel(MimoSe
     MPCQ_SSTAMP(1);
 
     // ---- setTransformations (:187-204): CS_d = sum_{k<=d} Cd Ad^k Bd (the distinct blocks of Su) and
-    // QCA_d = Q Cd Ad^(d+1) (for Fx = 2 (Sx' Qbar Su)', :307), by the recurrences AB_d = Ad AB_(d-1) and
-    // QCA_d = QCA_(d-1) Ad four horizon steps per barrier: with Ad^1..Ad^4 at hand, steps d0 .. d0+3 all
-    // come from step d0 - 1 (N / 4 barriers, and no Ad^k history: the LDS of two plants per CU).
+    // QCA_d = Q Cd Ad^(d+1) (for Fx = 2 (Sx' Qbar Su)', :307).  By doubling: with Ad^2, Ad^4, Ad^8, Ad^16 at
+    // hand, AB_(d + 2^k) = Ad^(2^k) AB_d and QCA_(d + 2^k) = QCA_d Ad^(2^k) give 2^k new steps per round, so
+    // the N <= 32 steps take 5 rounds (one barrier each) instead of a step-by-step recurrence.
     double *QCAh = sm + S.QCAh;                         // QCA_d, [d][ny][nx]
     double *ABh = sm + S.ABh;                           // Ad^d Bd, [d][nx][nu]
-    double *Pw = sm + S.Pw4;                            // Ad^(s+1) at Pw + s nx^2, s = 0..3
+    double *Pw = sm + S.Pw4;                            // Ad^(2^(s+1)) at Pw + s nx^2, s = 0..3
     double *QC = CA;                                    // Q Cd (ny x nx)
     const int ann = nx * nx, anu = nx * nu, ayx = ny * nx;
-    for (int e = t; e < ann; e += T) Pw[e] = Ad[e];
+    // round r (r = 0..4) forms, each item a dot12 over LDS: Ad^(2^(r+1)) = (Ad^(2^r))^2 (r < 4), the AB steps
+    // [2^r, 2^(r+1)) from [0, 2^r) (Ad^(2^r) times them; r = 0: AB_1 = Ad Bd) and the QCA steps ... likewise
+    // one round behind (QCA_0 = QC Ad, QCA_1 = QC Ad^2 need QC: round 1)
     for (int e = t; e < ayx; e += T) QC[e] = dot12(Q + (e / nx) * ny, 1, Cd + e % nx, nx, ny);
     for (int e = t; e < anu; e += T) ABh[e] = Bd[e];
-    __syncthreads();
-    for (int e = t; e < ann; e += T) Pw[ann + e] = dot12(Ad + (e / nx) * nx, 1, Ad + e % nx, nx, nx);  // Ad^2
-    for (int e = t; e < ayx; e += T) QCAh[e] = dot12(QC + (e / nx) * nx, 1, Ad + e % nx, nx, nx);     // QCA_0
-    __syncthreads();
-    for (int e = t; e < 2 * ann; e += T) {  // Ad^3 = Ad^2 Ad, Ad^4 = Ad^2 Ad^2
-        const int k = e / ann, f = e % ann;
-        Pw[(2 + k) * ann + f] = dot12(Pw + ann + (f / nx) * nx, 1, (k ? Pw + ann : Ad) + f % nx, nx, nx);
-    }
-    __syncthreads();
-    for (int d0 = 1; d0 < N; d0 += 4) {  // steps d0 .. d0 + 3 from step d0 - 1
-        const int steps = N - d0 < 4 ? N - d0 : 4;
-        for (int it = t; it < steps * (anu + ayx); it += T) {
-            const int sdx = it / (anu + ayx), e = it % (anu + ayx);
-            const double *Ps = Pw + sdx * ann;  // Ad^(sdx + 1)
-            if (e < anu) {  // AB_(d0 + sdx) = Ad^(sdx+1) AB_(d0 - 1)
-                const int i = e / nu, c = e % nu;
-                ABh[(size_t)(d0 + sdx) * anu + e] = dot12(Ps + i * nx, 1, ABh + (size_t)(d0 - 1) * anu + c, nu, nx);
-            } else {        // QCA_(d0 + sdx) = QCA_(d0 - 1) Ad^(sdx+1)
-                const int f = e - anu, i = f / nx, c = f % nx;
-                QCAh[(size_t)(d0 + sdx) * ayx + f] = dot12(QCAh + (size_t)(d0 - 1) * ayx + i * nx, 1, Ps + c, nx, nx);
+    for (int r = 0; r <= 5; r++) {
+        __syncthreads();
+        const int h = 1 << r;                          // AB: steps [h, 2h) from [0, h)
+        const double *Ph = r == 0 ? Ad : Pw + (r - 1) * ann;  // Ad^h
+        const int nab = N > h ? (N - h < h ? N - h : h) : 0;
+        // QCA: round 1 forms steps 0, 1 from QC; round r >= 2 steps [2^(r-1), 2^r) from [0, 2^(r-1))
+        const int hq = r >= 2 ? 1 << (r - 1) : 0;
+        const int nqa = r == 1 ? (N < 2 ? N : 2) : (r >= 2 && N > hq ? (N - hq < hq ? N - hq : hq) : 0);
+        const int npw = (r < 4 && ((2 << r) < N || r == 0)) ? ann : 0;  // Ad^(2h): needed while 2h < N (Ad^2: QCA_1)
+        const int items = npw + nab * anu + nqa * ayx;
+        for (int it = t; it < items; it += T) {
+            if (it < npw) {
+                const int i = it / nx, c = it % nx;
+                Pw[r * ann + it] = dot12(Ph + i * nx, 1, Ph + c, nx, nx);
+            } else if (it < npw + nab * anu) {
+                const int f = it - npw, sdx = f / anu, e = f % anu, i = e / nu, c = e % nu;
+                ABh[(size_t)(h + sdx) * anu + e] = dot12(Ph + i * nx, 1, ABh + (size_t)sdx * anu + c, nu, nx);
+            } else {
+                const int f = it - npw - nab * anu, sdx = f / ayx, e = f % ayx, i = e / nx, c = e % nx;
+                if (r == 1) {  // QCA_0 = QC Ad, QCA_1 = QC Ad^2
+                    QCAh[(size_t)sdx * ayx + e] = dot12(QC + i * nx, 1, (sdx ? Pw : Ad) + c, nx, nx);
+                } else {       // QCA_(hq + sdx) = QCA_sdx Ad^hq (Ad^hq = Pw slot r - 2)
+                    QCAh[(size_t)(hq + sdx) * ayx + e] =
+                        dot12(QCAh + (size_t)sdx * ayx + i * nx, 1, Pw + (r - 2) * ann + c, nx, nx);
+                }
             }
         }
-        __syncthreads();
     }
+    __syncthreads();
     for (int it = t; it < N * ny * nu; it += T) {  // Cd Ad^d Bd
         const int d = it / (ny * nu), i = (it / nu) % ny, c = it % nu;
         CS[it] = dot12(Cd + i * nx, 1, ABh + (size_t)d * nx * nu + c, nu, nx);
@@ -320,12 +334,20 @@ __global__ __launch_bounds__(kMimoSetupThreads, 8) void mimo_setup_kernel(MimoSe
         }
         out[L.Fu + (dl * nu + c) * nu + r] = 2.0 * (R[r * nu + c] + acc);
     }
-    // Frs = -2 sum_{d <= N-1-j} (Q CS_d)' (Fr = -2 (Qbar Su)', :306, summed over the horizon blocks)
+    // Frs = -2 sum_{d <= N-1-j} (Q CS_d)' = -2 (Q PCS_(N-1-j))' with PCS_k = sum_{d<=k} CS_d (Fr = -2 (Qbar Su)',
+    // :306, summed over the horizon blocks): CS becomes its prefix in place (setH has read it), then one
+    // Q product per block
+    for (int e = t; e < ny * nu; e += T) {
+        double acc = 0.0;
+        for (int d = 0; d < N; d++) {
+            acc += CS[(size_t)d * ny * nu + e];
+            CS[(size_t)d * ny * nu + e] = acc;
+        }
+    }
+    __syncthreads();
     for (int it = t; it < n * ny; it += T) {
         const int j = it / (nu * ny), r = (it / ny) % nu, i = it % ny;
-        double acc = 0.0;
-        for (int d = 0; d <= N - 1 - j; d++) acc += dot12(Q + i * ny, 1, CS + (size_t)d * ny * nu + r, nu, ny);
-        out[L.Frs + it] = -2.0 * acc;
+        out[L.Frs + it] = -2.0 * dot12(Q + i * ny, 1, CS + (size_t)(N - 1 - j) * ny * nu + r, nu, ny);
     }
     __syncthreads();
     MPCQ_SSTAMP(4);
@@ -377,23 +399,20 @@ __global__ __launch_bounds__(kMimoSetupThreads, 8) void mimo_setup_kernel(MimoSe
         if (pass == 1) MPCQ_SSTAMP(9);
         double cmt = 0.0;
         if (t < n) cmt = colfull(t);
-        if ((t >> 6) == 2) {  // wave 2 (no column of its own), lane k = block k: A-norm block maxima and
-                              // their suffix / prefix maxima
-            const int k = t & 63;
-#pragma unroll
-            for (int c = 0; c < 4; c++) {  // (all four scans in flight; components >= nu are zero)
-                double w0 = 0.0, w1 = 0.0;  // max_r E(k,r) |K0(r,c)|, max_q |K0(c,q)| D(k,q)
-                if (k < N && c < nu)
-                    for (int q = 0; q < nu; q++) {
-                        w0 = fmax(w0, Ec[k * nu + q] * fabs(K0[q * nu + c]));
-                        w1 = fmax(w1, fabs(K0[c * nu + q]) * Dc[k * nu + q]);
-                    }
-                w0 = lane_suffix_max(w0, k);
-                w1 = lane_prefix_max(w1, k);
-                if (k < 32) {
-                    wk[k * 4 + c] = w0;
-                    wk[128 + k * 4 + c] = w1;
+        if ((t >> 6) >= 2 && (t >> 6) < 6) {  // waves 2..5 (no column of their own), wave 2 + c for component c,
+                                                // lane k = block k: A-norm block maxima, suffix / prefix maxima
+            const int k = t & 63, c = (t >> 6) - 2;  // (components >= nu are zero)
+            double w0 = 0.0, w1 = 0.0;  // max_r E(k,r) |K0(r,c)|, max_q |K0(c,q)| D(k,q)
+            if (k < N && c < nu)
+                for (int q = 0; q < nu; q++) {
+                    w0 = fmax(w0, Ec[k * nu + q] * fabs(K0[q * nu + c]));
+                    w1 = fmax(w1, fabs(K0[c * nu + q]) * Dc[k * nu + q]);
                 }
+            w0 = lane_suffix_max(w0, k);
+            w1 = lane_prefix_max(w1, k);
+            if (k < 32) {
+                wk[k * 4 + c] = w0;
+                wk[128 + k * 4 + c] = w1;
             }
         }
         if (pass > 0 && t < 128) {  // mean column norm of c D P D (previous pass's cost scaling)
@@ -462,6 +481,7 @@ __global__ __launch_bounds__(kMimoSetupThreads, 8) void mimo_setup_kernel(MimoSe
         out[L.SW + it] = acc;
     }
     MPCQ_SSTAMP(7);
+    if (a.stamps && t == 0) a.stamps[(size_t)pl * 16 + 15] = (long long)__builtin_amdgcn_s_memrealtime();
 #undef MPCQ_SSTAMP
 }
 

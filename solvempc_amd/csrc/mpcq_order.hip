@@ -35,7 +35,8 @@ constexpr int kOrderThreads = 1024, kOrderQPW = kOrderThreads / 4;
 __global__ __launch_bounds__(kOrderThreads) void order_key_kernel(int batch, int nx, int m, const double *__restrict__ X,
                                                                   const double *__restrict__ U,
                                                                   const double *__restrict__ kmap, double xref,
-                                                                  int *__restrict__ cnt, int *__restrict__ key)
+                                                                  int *__restrict__ cnt, int *__restrict__ key,
+                                                                  double *__restrict__ Xs, double *__restrict__ Us)
 {
     constexpr int KB = OrderBins::kBins, KS = OrderBins::kStride, RPT = OrderBins::kMaxRows / 4;
     __shared__ double k[OrderBins::kMaxRows * KS];
@@ -49,6 +50,17 @@ __global__ __launch_bounds__(kOrderThreads) void order_key_kernel(int batch, int
 #pragma unroll
     for (int t = 0; t < 8; t++) x[t] = t < nx ? X[(size_t)bb * nx + t] : 0.0;
     const double u = U[bb];
+    if (Xs && b < batch) {  // the step's X, U for its q, u on demand (coalesced here, not per QP in the tile kernel)
+        double xa = x[0], xb = x[4];  // components part, part + 4 (selects: no register index by thread)
+#pragma unroll
+        for (int t = 1; t < 4; t++) {
+            xa = part == t ? x[t] : xa;
+            xb = part == t ? x[t + 4] : xb;
+        }
+        if (part < nx) Xs[(size_t)b * nx + part] = xa;
+        if (part + 4 < nx) Xs[(size_t)b * nx + part + 4] = xb;
+        if (part == 0) Us[b] = u;
+    }
     __syncthreads();
     // rows part, part + 4, ... (interleaved: the four threads of a QP read different rows of one LDS line)
     double v = -__builtin_inf();
@@ -117,16 +129,17 @@ __global__ __launch_bounds__(256) void order_scatter_kernel(int batch, const int
 }  // namespace mpcq
 
 // cnt: OrderBins::kBins counters, zero on entry (cleared by the previous ordered tile launch, or by the
-// caller); key: batch ints of scratch; list: batch ints, the QPs hardest first.
+// caller); key: batch ints of scratch; list: batch ints, the QPs hardest first; Xs, Us (or null): copies of
+// X, U (the tile kernel's X_save, U_save, which the ordered launch then leaves to this kernel).
 extern "C" int mpcq_internal_order(int batch, int nx, int m, const double *X, const double *U, const double *kmap,
-                                   double xref, int *cnt, int *key, int *list, hipStream_t s)
+                                   double xref, int *cnt, int *key, int *list, double *Xs, double *Us, hipStream_t s)
 {
     if (batch <= 0 || batch >= (1 << mpcq::OrderBins::kRankBits) || nx <= 0 || nx > 8 || m <= 0 ||
         m > mpcq::OrderBins::kMaxRows)
         return -1;
     const int blocks = (batch + 255) / 256;
     hipLaunchKernelGGL(mpcq::order_key_kernel, dim3((batch + mpcq::kOrderQPW - 1) / mpcq::kOrderQPW),
-                       dim3(mpcq::kOrderThreads), 0, s, batch, nx, m, X, U, kmap, xref, cnt, key);
+                       dim3(mpcq::kOrderThreads), 0, s, batch, nx, m, X, U, kmap, xref, cnt, key, Xs, Us);
     if (hipGetLastError() != hipSuccess) return -2;
     hipLaunchKernelGGL(mpcq::order_scatter_kernel, dim3(blocks), dim3(256), 0, s, batch, (const int *)cnt,
                        (const int *)key, list);

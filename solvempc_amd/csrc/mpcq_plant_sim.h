@@ -40,7 +40,9 @@ __device__ __forceinline__ double sim_row(int i, int nx, const double *A, const 
 {
     const int np = (nx + 1) / 2;  // Box-Muller pairs: w[t] = r_t cos th_t (t < np), r_{t-np} sin th_{t-np}
     double s = 0.0;
-    for (int t = 0; t < nx; t++) s += A[i * nx + t] * x[t];
+#pragma unroll
+    for (int t = 0; t < 8; t++)  // (unrolled over the capacity: x stays in registers, no dynamic index)
+        if (t < nx) s += A[i * nx + t] * x[t];
     s += B[i] * u;
     double w = 0.0;
     if (noise_std != 0.0) {

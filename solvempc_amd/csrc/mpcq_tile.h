@@ -225,13 +225,23 @@ __device__ __forceinline__ float rem_reduce(const Mf<float>::acc &p)
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);                // row g
 }
 
+// Optional accumulator init of the products below: a [G][4 NTO] array, or nullptr (a compile-time choice:
+// a runtime null test on a private array's address cannot fold -- private address 0 is valid -- and would
+// keep the array in scratch memory)
+template <typename IT> constexpr bool kHasInit = !std::is_same<IT, std::nullptr_t>::value;
+template <typename T, typename IT> __device__ __forceinline__ T init_el(IT p, int gi, int k)
+{
+    if constexpr (kHasInit<IT>) return p[gi][k];
+    else return T(0);
+}
+
 // The same product for G independent 16-QP groups of one wave: every A operand read from LDS feeds
 // G MFMAs, and the G accumulator chains interleave (more independent work per wave).
 // REM (f32, the last tile holds 4 real rows): that tile on v_mfma_f32_4x4x1_16b, its A fragment read
 // from the 16x16x4 image's lane (g, 4 (c & 3)) (see reg_mv), then rem_reduce; init added after it.
-template <typename T, int G, int NTO, int KS, int KSP, int XN, bool REM = false>
+template <typename T, int G, int NTO, int KS, int KSP, int XN, bool REM = false, typename IT = std::nullptr_t>
 __device__ __forceinline__ void tile_mv_g(const T *__restrict__ im, const T (&x)[G][XN], T (&y)[G][4 * NTO],
-                                          int lane, const T (*init)[4 * NTO])
+                                          int lane, IT init)
 {
     using A = typename Mf<T>::acc;
     constexpr int VEC = 16 / sizeof(T);
@@ -253,7 +263,7 @@ __device__ __forceinline__ void tile_mv_g(const T *__restrict__ im, const T (&x)
 #pragma unroll
         for (int t = 0; t < NTO; t++)
 #pragma unroll
-            for (int r = 0; r < 4; r++) acc[gi][t][r] = (init && t < NF) ? init[gi][4 * t + r] : T(0);
+            for (int r = 0; r < 4; r++) acc[gi][t][r] = (kHasInit<IT> && t < NF) ? init_el<T>(init, gi, 4 * t + r) : T(0);
 #pragma unroll
     for (int s = 0; s < KS; s++)
 #pragma unroll
@@ -278,7 +288,7 @@ __device__ __forceinline__ void tile_mv_g(const T *__restrict__ im, const T (&x)
                     if (t == NF) {
                         if (r == 0) {
                             const T v = rem_reduce(acc[gi][t]);
-                            y[gi][4 * t] = init ? v + init[gi][4 * t] : v;
+                            y[gi][4 * t] = kHasInit<IT> ? v + init_el<T>(init, gi, 4 * t) : v;
                         } else {
                             y[gi][4 * t + r] = T(0);
                         }
@@ -299,9 +309,10 @@ __device__ __forceinline__ void tile_mv_g(const T *__restrict__ im, const T (&x)
 // RMODE (REM only) defers the remainder tile's lane reduction across two products: 1 = leave its
 // 4x4x1 partial sums unreduced in rem[] and put init's remainder element (not the product's) into y;
 // 2 = start the remainder chain from rem[] (the partials of a mode-1 product), reduce, add init.
-template <typename T, int G, int NTO, int KS, int XN, bool TWO, int XN2, bool REM = false, int RMODE = 0>
+template <typename T, int G, int NTO, int KS, int XN, bool TWO, int XN2, bool REM = false, int RMODE = 0,
+          typename IT = std::nullptr_t>
 __device__ __forceinline__ void reg_mv(const T (&m1)[NTO][KS], const T (&x1)[G][XN], const T (&m2)[NTO][KS],
-                                       const T (&x2)[G][XN2], T (&y)[G][4 * NTO], const T (*init)[4 * NTO],
+                                       const T (&x2)[G][XN2], T (&y)[G][4 * NTO], IT init,
                                        typename Mf<T>::acc *rem = nullptr)
 {
     using A = typename Mf<T>::acc;
@@ -315,7 +326,8 @@ __device__ __forceinline__ void reg_mv(const T (&m1)[NTO][KS], const T (&x1)[G][
         for (int t = 0; t < NTO; t++)
 #pragma unroll
             for (int r = 0; r < 4; r++)
-                acc[gi][t][r] = (init && t < NF) ? init[gi][4 * t + r] : ((RMODE == 2 && t == NF) ? rem[gi][r] : T(0));
+                acc[gi][t][r] = (kHasInit<IT> && t < NF) ? init_el<T>(init, gi, 4 * t + r)
+                                                         : ((RMODE == 2 && t == NF) ? rem[gi][r] : T(0));
     auto step = [&](const T (&m)[NTO][KS], auto &x, int s) {
 #pragma unroll
         for (int t = 0; t < NTO; t++)
@@ -345,7 +357,7 @@ __device__ __forceinline__ void reg_mv(const T (&m1)[NTO][KS], const T (&x1)[G][
                 if constexpr (REM && RMODE == 1) {
                     if (t == NF) {
                         if (r == 0) rem[gi] = acc[gi][t];
-                        y[gi][4 * t + r] = (init && r == 0) ? init[gi][4 * t] : T(0);
+                        y[gi][4 * t + r] = (kHasInit<IT> && r == 0) ? init_el<T>(init, gi, 4 * t) : T(0);
                         continue;
                     }
                 }
@@ -353,7 +365,7 @@ __device__ __forceinline__ void reg_mv(const T (&m1)[NTO][KS], const T (&x1)[G][
                     if (t == NF) {
                         if (r == 0) {
                             const T v = rem_reduce(acc[gi][t]);
-                            y[gi][4 * t] = init ? v + init[gi][4 * t] : v;
+                            y[gi][4 * t] = kHasInit<IT> ? v + init_el<T>(init, gi, 4 * t) : v;
                         } else {
                             y[gi][4 * t + r] = T(0);
                         }
@@ -412,6 +424,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
     // q^ of each wave's QPs (lane layout): the dual residual of every check iteration reads it here
     // instead of re-reading q (fp64, HBM) under the latency of a loaded memory system
     __shared__ T s_qh[WPB][G * KN][64];
+    // stream (STREAM): every column's plant state X (8), U, in LDS rather than in VGPRs held across the
+    // solve (the check and refill code of the stream instantiation spilled); all four lanes of a column
+    // read and write the same values (one wave: its DS instructions execute in order)
+    __shared__ double s_plant[STREAM ? WPB * 16 * 9 : 1];
     T *const s_lam = rowv, *const s_D = rowv + NCP, *const s_Dinv = rowv + 2 * NCP;
     T *const s_E = rowv + 3 * NCP, *const s_Einv = rowv + 3 * NCP + MCP;
     // resumed phase: this workgroup serves list segment `seg` (ListSeg), as its workgroup `blk`
@@ -557,9 +573,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
         kst[gi] = 0;
         over[gi] = !valid[gi];
     }
-    double sX[8], sU = 0.0;  // stream: the column's plant state X, U (every lane of the column holds it)
-#pragma unroll
-    for (int t = 0; t < 8; t++) sX[t] = 0.0;
+    double *const pst = s_plant + (STREAM ? ((threadIdx.x >> 6) * 16 + c) * 9 : 0);  // stream: X[0..8), U
     // ---- per-QP data of the columns in `fill` (element v = 4 s + g of this lane's QP column), per
     // group: every column at entry, the refilled ones at a check (the others keep their registers and
     // reproduce their W' q^ bit for bit).  Every global load of a group is issued (index clamped into
@@ -577,10 +591,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             double Xv[8];
             const int nx = a.nx;
             double Uv;
-            if (refill && !entry) {  // a stream column's later step: its plant state is in registers
+            if (refill && !entry) {  // a stream column's later step: its plant state is in LDS
 #pragma unroll
-                for (int t = 0; t < 8; t++) Xv[t] = sX[t];
-                Uv = sU;
+                for (int t = 0; t < 8; t++) Xv[t] = pst[t];
+                Uv = pst[8];
             } else {
 #pragma unroll
                 for (int t = 0; t < 8; t++) Xv[t] = a.X[(size_t)b * nx + (t < nx ? t : 0)];
@@ -590,8 +604,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                     if (t >= nx) Xv[t] = 0.0;
                 if (refill) {
 #pragma unroll
-                    for (int t = 0; t < 8; t++) sX[t] = Xv[t];
-                    sU = Uv;
+                    for (int t = 0; t < 8; t++) pst[t] = Xv[t];
+                    pst[8] = Uv;
                 }
             }
 #pragma unroll
@@ -773,6 +787,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
         for (int gi = 0; gi < G; gi++) {
             if (!mine[gi]) continue;
             const int b = opaque(b_[gi]);
+            // (the lane's row offset and the output pointers re-derived here: per-pointer lane addresses are
+            // not hoisted out of the finalize and held, as 64-bit VGPR pairs, across the hot loop)
+            const int g = opaque((int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u))) >> 4;
+            T *const o_xs = fresh_ptr(a.xs), *const o_zs = fresh_ptr(a.zs), *const o_ys = fresh_ptr(a.ys);
+            T *const o_rhos = fresh_ptr(a.rhos);
+            int *const o_status = fresh_ptr(a.status), *const o_iter = fresh_ptr(a.iter);
+            double *const o_rho = fresh_ptr(a.rho_out), *const o_U = fresh_ptr(a.U);
             const int sta = status[gi];
             const bool has_sol = sta == kSolved || sta == kSolvedInaccurate || sta == kMaxIterReached;
             // a stream column between two of its control steps keeps the solver state in registers
@@ -784,13 +805,14 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 if (s < KN && v < n) {
                     const double xv = has_sol ? (double)xh[gi][s] * (double)s_D[v] : __builtin_nan("");
                     if (a.x && full) a.x[(size_t)b * n + v] = xv;
-                    if (!refill && v == 0 && a.mpc_u && sta == kSolved) a.U[b] = (Uold ? Uold[gi] : a.U[b]) + xv;  // U += x(0)  (:105)
+                    if (!refill && v == 0 && a.mpc_u && sta == kSolved) o_U[b] = (Uold ? Uold[gi] : o_U[b]) + xv;  // U += x(0)  (:105)
                 }
             }
             if (refill) {  // stream: U += x(0) on every lane of the column (x(0): lane group 0, register 0)
                 const double x0 = col_from(has_sol ? (double)xh[gi][0] * (double)s_D[0] : 0.0, 0, g);
-                if (a.mpc_u && sta == kSolved) sU = sU + x0;
-                if (full && g == 0) a.U[b] = sU;
+                const double u1 = (a.mpc_u && sta == kSolved) ? pst[8] + x0 : pst[8];
+                pst[8] = u1;
+                if (full && g == 0) o_U[b] = u1;
             }
             const bool keep = has_sol || sta == kInvalidBounds || sta == kTypeChanged;
             if (!full) {
@@ -814,18 +836,19 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             }
 #pragma unroll
             for (int s = 0; s < NS; s++)
-                if (s < KN) a.xs[(size_t)b * ncs + 4 * s + g] = keep ? xs[gi][s] : T(0);
+                if (s < KN) o_xs[(size_t)b * ncs + 4 * s + g] = keep ? xs[gi][s] : T(0);
 #pragma unroll
             for (int s = 0; s < MS; s++)
                 if (s < KM) {
-                    a.zs[(size_t)b * mcs + 4 * s + g] = keep ? z[gi][s] : T(0);
-                    a.ys[(size_t)b * mcs + 4 * s + g] = keep ? y[gi][s] : T(0);
+                    o_zs[(size_t)b * mcs + 4 * s + g] = keep ? z[gi][s] : T(0);
+                    o_ys[(size_t)b * mcs + 4 * s + g] = keep ? y[gi][s] : T(0);
                 }
             if (g == 0) {
-                a.rhos[b] = rho[gi];
-                a.status[b] = sta;
-                a.iter[b] = it - cst[gi];
-                a.rho_out[b] = (double)rho[gi];
+                o_rhos[b] = rho[gi];
+                o_status[b] = sta;
+                o_iter[b] = it - cst[gi];
+                if (a.rho_out) o_rho[b] = (double)rho[gi];  // (null: the fp64 rhos above is reported, mpcq_api.cpp
+                                                            // materialize_rho)
                 if (a.it_acc) {
                     a.it_acc[b] += it - cst[gi];
                     a.uns_acc[b] += sta != kSolved;
@@ -855,14 +878,17 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 const double *Bd = a.sim.Bd + (a.sim.shared ? 0 : (size_t)b * nx);
                 const unsigned long long key = sim_key(a.sim.seed), idx = (unsigned long long)(a.sim.first_qp + b);
                 const long long step = a.sim.first_step + kst[0];
-                double x0 = 0.0, x1 = 0.0;
+                double x0 = 0.0, x1 = 0.0, sX[8];
+#pragma unroll
+                for (int t = 0; t < 8; t++) sX[t] = pst[t];
+                const double sU = pst[8];
                 if (fin && g < nx) x0 = sim_row(g, nx, Ad, Bd, sX, sU, key, idx, step, a.sim.noise_std);
                 if (fin && g + 4 < nx) x1 = sim_row(g + 4, nx, Ad, Bd, sX, sU, key, idx, step, a.sim.noise_std);
                 // the new X on every lane of the column (component t from lane group t & 3)
 #pragma unroll
                 for (int t = 0; t < 8; t++) {
                     const double v = col_from(t < 4 ? x0 : x1, t & 3, g);
-                    if (fin) sX[t] = t < nx ? v : 0.0;
+                    if (fin) pst[t] = t < nx ? v : 0.0;
                 }
                 bool fill[G];
                 fill[0] = fin && kst[0] + 1 < a.sim.steps;
@@ -1032,7 +1058,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
 #pragma unroll
             for (int k = 0; k < KNR; k++) rBS[t][k] = im[L.BS + TileLayout::at(KNP, VEC, t, k, lane)];
     };
-    auto piter_stk = [&](const T (&rBt)[NTR][KNR], const T (&rBS)[NBR][KNR], T (&sx)[G][NS], const T (&adk)[G][KNR]) {
+    auto piter_stk = [&](const T (&rBt)[NTR][KNR], const T (&rBS)[NBR][KNR], T (&sx)[G][NS], const T (&adk)[G][KNR],
+                         const T (&agv)[G][KNR]) {
         if constexpr (NBS > 0) {
             T wt[G][KNR];
 #pragma unroll
@@ -1047,7 +1074,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             for (int gi = 0; gi < G; gi++)
 #pragma unroll
                 for (int f = 0; f < 4 * NBR; f++)
-                    ini[gi][f] = (f >= KN && f < 2 * KN) ? tt_fma(oma, sx[gi][f - KN], alpha * gv[gi][f - KN]) : T(0);
+                    ini[gi][f] = (f >= KN && f < 2 * KN) ? tt_fma(oma, sx[gi][f - KN], agv[gi][f - KN]) : T(0);
 #pragma unroll
             for (int gi = 0; gi < G; gi++)
 #pragma unroll
@@ -1233,12 +1260,15 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                         for (int s = 0; s < NS; s++) {
                             xs32[gi][s] = (float)xs[gi][s];
                             gv32[gi][s] = (float)gv[gi][s];
+                            asm volatile("" : "+v"(gv32[gi][s]));  // (as uh32 below)
                         }
 #pragma unroll
                         for (int s = 0; s < MS; s++) {
                             z32[gi][s] = (float)z[gi][s];
                             y32[gi][s] = s < KM ? (float)(y[gi][s] * rinv[gi]) : 0.0f;
                             uh32[gi][s] = (float)uh[gi][s];
+                            // (the fp32 bounds are values of their own: not re-converted from uh inside the loop)
+                            asm volatile("" : "+v"(uh32[gi][s]));
                         }
 #pragma unroll
                         for (int s = 0; s < KN; s++) adk32[gi][s] = (float)(alpha * dk[gi][s]);
@@ -1285,18 +1315,23 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 if (it + 1 < nxt) {
                     T rBt[NTR][KNR], rBS[NBR][KNR];
                     load_regs_stk(rBt, rBS);
-                    T sx[G][NS], adk[G][KNR];
+                    T sx[G][NS], adk[G][KNR], agv[G][KNR];
                     tile_mv_g<T, G, NT, KN, KNP>(img + L.S, xs, sx, lane, gv);  // -g + S x'
 #pragma unroll
                     for (int gi = 0; gi < G; gi++) {
 #pragma unroll
-                        for (int s = 0; s < KN; s++) adk[gi][s] = alpha * dk[gi][s];
+                        for (int s = 0; s < KN; s++) {
+                            // (loop invariants of their own: not recomputed inside the loop)
+                            adk[gi][s] = alpha * dk[gi][s];
+                            agv[gi][s] = alpha * gv[gi][s];
+                            asm volatile("" : "+v"(adk[gi][s]), "+v"(agv[gi][s]));
+                        }
 #pragma unroll
                         for (int s = 0; s < KM; s++) y[gi][s] = y[gi][s] * rinv[gi];  // y -> yt = y / rho
                     }
                     do {
                         it++;
-                        piter_stk(rBt, rBS, sx, adk);
+                        piter_stk(rBt, rBS, sx, adk, agv);
                     } while (it + 1 < nxt);
 #pragma unroll
                     for (int gi = 0; gi < G; gi++)
@@ -1681,8 +1716,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
         };
         // check_termination(approximate) — OSQP auxil.c; new status per group (kUnsolved: go on)
         auto check_termination = [&](bool approx, const bool (&need0)[G], int (&out)[G]) {
-            const T mul = approx ? T(10) : T(1);
-            const T ea = eps_abs * mul, er = eps_rel * mul;
+            // (the approximate check's 10 eps from the arguments, formed on the host in T: products hoisted
+            // out of the loop would be held, and spilled, in VGPRs)
+            const T ea = approx ? a.eps10[0] : eps_abs, er = approx ? a.eps10[1] : eps_rel;
             bool noncvx[G], prim_ok[G], dual_ok[G], need_p[G], need_d[G], prim_inf[G], dual_inf[G];
 #pragma unroll
             for (int gi = 0; gi < G; gi++) {
@@ -1700,8 +1736,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 dual_ok[gi] = dua_res[gi] < ed;
                 need_d[gi] = need && !dual_ok[gi];
             }
-            primal_infeasible((T)st.eps_prim_inf * mul, need_p, prim_inf);
-            dual_infeasible((T)st.eps_dual_inf * mul, need_d, dual_inf);
+            primal_infeasible(approx ? a.eps10[2] : (T)st.eps_prim_inf, need_p, prim_inf);
+            dual_infeasible(approx ? a.eps10[3] : (T)st.eps_dual_inf, need_d, dual_inf);
 #pragma unroll
             for (int gi = 0; gi < G; gi++) {
                 int o = kUnsolved;
@@ -1787,19 +1823,23 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             for (int gi = 0; gi < G; gi++) {
                 const bool run = !done[gi];
                 const int b = opaque(b_[gi]);
+                // (lane offset and pointers re-derived here, as in the finalize: nothing of this cold path is
+                // hoisted and held across the hot loop)
+                const int g = opaque((int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u))) >> 4;
+                T *const o_xs = fresh_ptr(a.xs), *const o_zs = fresh_ptr(a.zs), *const o_ys = fresh_ptr(a.ys);
                 if (run) {
 #pragma unroll
                     for (int s = 0; s < NS; s++)
-                        if (s < KN) a.xs[(size_t)b * ncs + 4 * s + g] = xs[gi][s];
+                        if (s < KN) o_xs[(size_t)b * ncs + 4 * s + g] = xs[gi][s];
 #pragma unroll
                     for (int s = 0; s < MS; s++)
                         if (s < KM) {
-                            a.zs[(size_t)b * mcs + 4 * s + g] = z[gi][s];
-                            a.ys[(size_t)b * mcs + 4 * s + g] = y[gi][s];
+                            o_zs[(size_t)b * mcs + 4 * s + g] = z[gi][s];
+                            o_ys[(size_t)b * mcs + 4 * s + g] = y[gi][s];
                         }
                     if (g == 0) {
-                        a.rhos[b] = rho[gi];
-                        a.it_state[b] = it;
+                        fresh_ptr(a.rhos)[b] = rho[gi];
+                        fresh_ptr(a.it_state)[b] = opaque(it);  // (it == stop here: no VGPR copy of stop held)
                     }
                 }
             }
@@ -1816,8 +1856,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
             int *const qout = a.list_out + (blockIdx.x % ListSeg::kShards) * a.list_seg;
 #pragma unroll
             for (int gi = 0; gi < G; gi++) {
-                const unsigned long long below = (1ull << c) - 1ull;  // the column's g = 0 lane is lane c
-                int pos = base + __popcll(mask[gi] & below);
+                // the column's g = 0 lane is lane c: the mask's bits below it by mbcnt (no lane mask held)
+                int pos = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask[gi] >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((unsigned)mask[gi], 0u));
 #pragma unroll
                 for (int gj = 0; gj < gi; gj++) pos += __popcll(mask[gj]);
                 if (!done[gi] && g == 0) qout[pos] = opaque(b_[gi]);
@@ -1877,17 +1918,25 @@ int tile_stream_launch(const AdmmArgs<T> &a, hipStream_t s)
 {
     if constexpr (KM == 2 * KN) {
         if (a.paired && a.all_ineq && a.lower_free) {
-            constexpr int OCC = 2, WPB = 4;  // (a stream is latency-bound: few waves, no spills)
+            // (a stream is latency-bound: few waves.  Compiled for two waves per SIMD (its plant and check code
+            // spill, outside the hot loop), or with StreamArgs::occ 1 for one: the whole register file, no
+            // spills, but slower (mpcq_api.cpp launch_tile_stream))
+            constexpr int WPB = 4;
             const int waves = (a.batch + a.sim.cpw - 1) / a.sim.cpw;
+            const dim3 grid((waves + WPB - 1) / WPB), block(64 * WPB);
             if constexpr (std::is_same<T, double>::value) {
                 if (a.mix_r > 0) {  // MPCQ_F64_MIXED: each step's plain iterations before the last mix_r in fp32
-                    hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 1, OCC, true, WPB, true, true>),
-                                       dim3((waves + WPB - 1) / WPB), dim3(64 * WPB), 0, s, a);
+                    if (a.sim.occ == 1)
+                        hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 1, 1, true, WPB, true, true>), grid, block, 0, s, a);
+                    else
+                        hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 1, 2, true, WPB, true, true>), grid, block, 0, s, a);
                     return hipGetLastError() == hipSuccess ? 0 : -2;
                 }
             }
-            hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 1, OCC, true, WPB, true>),
-                               dim3((waves + WPB - 1) / WPB), dim3(64 * WPB), 0, s, a);
+            if (a.sim.occ == 1)
+                hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 1, 1, true, WPB, true>), grid, block, 0, s, a);
+            else
+                hipLaunchKernelGGL((admm_tile_kernel<T, KN, KM, true, true, 1, 2, true, WPB, true>), grid, block, 0, s, a);
             return hipGetLastError() == hipSuccess ? 0 : -2;
         }
     }

@@ -2,6 +2,7 @@
 # One GPU call of round 5: the GPU test suite, the default bench line and optional extras, each step under its
 # own time limit, stopping at the first failure.  Usage: tools/gpu_r05.sh TAG [steps...]
 #   steps: tests | tests:<pytest -k expr> | bench | bench:<args> | probe:<dtype> | smoke | prof | pmc:<counters>
+#          | envbench:VAR=val,<args> | pmcw:VAR=val,<dtype> | stamps:mimo_setup | tstamps:<dtype> | calib
 set -o pipefail
 tag=$1; shift
 out=gpurun_out/$tag
@@ -37,9 +38,26 @@ for step in "$@"; do
              # beforehand (SRC=mpcq_mimo.hip DBGDIR=tools/dbg_r05 bash tools/build_dbg.sh)
       MPCQ_LIBRARY=tools/dbg_r05/libmpcq.so timeout -k 10 300 python -u tools/mimo_setup_stamps.py > "$out/stamps_$arg.log" 2>&1 \
         || { echo "stamps failed"; tail "$out/stamps_$arg.log"; exit 1; } ;;
+    tstamps)  # tstamps:<dtype> -> per-wave stage stamps of the tile kernel (debug library tools/dbg_r05t, built
+              # here: SRC=mpcq_tile_f64.hip DBGDIR=tools/dbg_r05t bash tools/build_dbg.sh MPCQ_INFO_STAMPS)
+      MPCQ_LIBRARY=tools/dbg_r05t/libmpcq.so MPCQ_TILE_STAMPS="$out/tstamps_$arg.bin" timeout -k 10 300 \
+        python bench.py --dtype $arg --steps 1 --warmup 1 --cpu-seconds 0 --variants 0 > "$out/tstamps_bench_$arg.json" 2>&1 \
+        && python tools/stamps.py "$out/tstamps_$arg.bin" > "$out/tstamps_$arg.txt" 2>&1 \
+        || { echo "tstamps failed"; tail "$out/tstamps_bench_$arg.json"; exit 1; } ;;
     calib)  # WRITE_SIZE calibration of the finalize's store patterns (tools/calib/write_calib.hip, built here)
       (cd "$out" && timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d calib -o run -- "$GRAFT_REPO_ROOT/tools/calib/write_calib" \
         > calib.log 2>&1) || { echo "calib failed"; tail "$out/calib.log"; exit 1; } ;;
+    envbench)  # envbench:VAR=val,<bench args with _ for spaces> -> 3 bench lines with the test hook set
+      IFS=, read -r ev rest <<< "$arg"
+      for r in 1 2 3; do
+        env "$ev" timeout -k 10 300 python -u bench.py ${rest//_/ } --cpu-seconds 0 --variants 0 > "$out/eb_${ev}_$r.json" 2> "$out/eb.err" \
+          || { echo "envbench failed"; tail -20 "$out/eb.err"; exit 1; }
+      done ;;
+    pmcw)  # pmcw:VAR=val,<dtype> -> one WRITE_SIZE pass of the cfg2 bench with the test hook set
+      IFS=, read -r ev dt <<< "$arg"
+      env "$ev" CMD="python bench.py --dtype $dt --steps 3 --warmup 1 --cpu-seconds 0 --variants 0" PMC_SETS=WRITE_SIZE \
+        timeout -k 10 300 bash tools/pmc.sh "$dt" "$out/pmcw_${ev}_$dt" > "$out/pmcw_${ev}_$dt.log" 2>&1 \
+        || { echo "pmcw failed"; cat "$out/pmcw_${ev}_$dt/passes.txt"; exit 1; } ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   echo "step $step ok"

@@ -43,3 +43,17 @@ for k in range(1, 8):
 for k, nm in ((9, "pass-1 first barrier"), (10, "pass-1 A norms + cost"), (11, "pass-1 D, E update")):
     d = h[:, k] - h[:, k - 1]
     print(f"  {nm:22s} median {np.median(d):8.0f}")
+
+# co-residency: workgroups of one CU (HW_ID cu/sh/se fields + XCC) overlapping in s_memrealtime (100 MHz)
+hw, xcc, t0, t1 = h[:, 12], h[:, 13], h[:, 14], h[:, 15]
+cu = (xcc & 0xF) * 4096 + ((hw >> 8) & 0xF) + 16 * ((hw >> 12) & 0x1) + 32 * ((hw >> 13) & 0x7)
+ev = np.concatenate([np.stack([t0, np.ones_like(t0), cu], 1), np.stack([t1, -np.ones_like(t1), cu], 1)])
+ev = ev[np.lexsort((ev[:, 1], ev[:, 0]))]
+from collections import defaultdict
+live, peak = defaultdict(int), defaultdict(int)
+for tt, d, c in ev:
+    live[c] += d
+    peak[c] = max(peak[c], live[c])
+pk = np.array(list(peak.values()))
+print(f"CUs seen {len(pk)}; workgroups resident at once per CU: max {pk.max()} median {np.median(pk):.0f}")
+print(f"kernel span {(t1.max() - t0.min()) / 100:.0f} us; mean workgroup {(t1 - t0).mean() / 100:.1f} us")
