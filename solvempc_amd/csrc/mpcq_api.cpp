@@ -52,6 +52,7 @@ constexpr int kMaxPhases = 16;
 //   MPCQ_MIX_R=r                MPCQ_F64_MIXED: fp64 iterations per check interval (default MPCQ_MIX_R)
 //   MPCQ_TILE_OCC=2|3           waves per SIMD of the f32 paired tile kernel (default 3)
 //   MPCQ_PLANT_WPE=2|3|4        waves per SIMD of the one-pass per-plant kernel (default f64 3, f32 2)
+//   MPCQ_PLANT_LAYOUT=2         the one-pass per-plant kernel with two plants per wave at N 17 .. 20 (default 3)
 //   MPCQ_ORDER=0                a shared-plant MPC step's tile solve in index order (default: hardest first)
 //   MPCQ_LAZY_XY=0              the tile solve stores x, y at finalize (default: published on demand)
 // Debug builds (-DMPCQ_DEBUG_HOOKS) add the stamp / profiling dumps (MPCQ_TILE_STAMPS,
@@ -1771,6 +1772,8 @@ int mpcq_mpc_plants_step_device(mpcq_ctx *c, int nx, int s_rows, const double *A
         // 35.5-35.9 M at 2), fp32 at 2 (3 spills into its loop: slower); MPCQ_PLANT_WPE=2|3 for A/B
         const char *w = test_hook("MPCQ_PLANT_WPE");
         a.wpe = *w ? std::atoi(w) : (c->dims.dtype == MPCQ_F32 ? 2 : 3);
+        const char *l = test_hook("MPCQ_PLANT_LAYOUT");  // 2: two plants per wave at N 17 .. 20 (A/B, parity)
+        a.layout = *l ? std::atoi(l) : 0;
     }
     const int lr = mpcq_internal_plant_step_launch(&a, c->dims.dtype == MPCQ_F32, s);
     if (lr) return fail(lr == -1 ? MPCQ_ERR_ARG : MPCQ_ERR_HIP, "plants_step kernel launch failed");

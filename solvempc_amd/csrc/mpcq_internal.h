@@ -380,6 +380,8 @@ struct PlantStepArgs {
     int *status, *iter;
     int *flags;                                    // OR: 1 a plant's KKT matrix is not positive definite
     int wpe;                                       // waves per SIMD of the kernel variant (2; 3: A/B hook)
+    int layout;                                    // plants per wave (0: the default, 3 for 17 <= N <= 20;
+                                                   // 2: one per 32-lane half, test hook MPCQ_PLANT_LAYOUT)
 };
 }  // namespace mpcq
 

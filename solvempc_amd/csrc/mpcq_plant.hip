@@ -151,11 +151,173 @@ template <typename T> __device__ __forceinline__ T ssum(T v, int lane)
     return half_suffix(v, [](T a, T b) { return a + b; }, lane);
 }
 
+// ---- plants per wave (LAY).  LAY 2: two plants, one per 32-lane half, lane r of a half = horizon step r
+// (the functions above).  LAY 3 (N <= 20): three plants, plant h on row h (lanes 16 h .. 16 h + 15: steps
+// 0 .. 15) and steps 16 .. 19 interleaved over row 3 (step 16 + k at lane 48 + 4 k + h; lanes 48 + 4 k + 3
+// hold no plant), so 60 of 64 lanes carry a step.  The scans and reductions keep the association of the
+// two-plant layout: the row part runs the same DPP steps (rows 0 .. 2 only where row 3 would mix plants),
+// the interleaved steps 16 .. 19 combine with row shifts by 4 and 8 lanes (one step apart, two steps
+// apart), and the carry between a plant's row and its tail crosses rows by ds_bpermute (the LDS crossbar:
+// no VALU issue).  Lanes of no plant hold 0 in every scan input (their predicates are false), and lane 63
+// is the zero every other lane's carry reads; they count in plant 2's slot and take plant 2's reductions,
+// so their decisions (status, `done`) are plant 2's.
+__device__ __forceinline__ int lay3_plant(int lane) { return lane < 48 ? lane >> 4 : ((lane & 3) == 3 ? 2 : lane & 3); }
+__device__ __forceinline__ int lay3_row(int lane) { return lane < 48 ? lane & 15 : ((lane & 3) == 3 ? 32 : 16 + ((lane >> 2) & 3)); }
+template <int LAY> __device__ __forceinline__ int lay_plant(int lane) { return LAY == 3 ? lay3_plant(lane) : lane >> 5; }
+template <int LAY> __device__ __forceinline__ int lay_row(int lane) { return LAY == 3 ? lay3_row(lane) : lane & 31; }
+
+// DPP move under row / bank masks: lanes of a disabled row or bank keep `old`; bound_ctrl: a lane whose
+// source lies outside its row reads 0
+template <int CTRL, int RM, int BM> __device__ __forceinline__ float dppm(float old, float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL, RM, BM, true));
+}
+template <int CTRL, int RM, int BM> __device__ __forceinline__ double dppm(double old, double v)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v), o = (unsigned long long)__double_as_longlong(old);
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)o, (int)(unsigned)u, CTRL, RM, BM, true);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)(o >> 32), (int)(unsigned)(u >> 32), CTRL, RM, BM, true);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// the value of v at lane src (src4 = 4 src): ds_bpermute
+__device__ __forceinline__ float lane_fetch(float v, int src4)
+{
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(src4, __float_as_int(v)));
+}
+__device__ __forceinline__ double lane_fetch(double v, int src4)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_ds_bpermute(src4, (int)(unsigned)u);
+    const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute(src4, (int)(unsigned)(u >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// LAY 3 inclusive prefix / suffix over a plant's steps (op with identity 0, as half_prefix / half_suffix)
+template <typename T, typename F> __device__ __forceinline__ T lay3_prefix(T v, F op, int lane)
+{
+    v = op(v, dppm<0x111, 0x7, 0xF>(T(0), v));  // row_shr 1, 2: rows 0 .. 2 only
+    v = op(v, dppm<0x112, 0x7, 0xF>(T(0), v));
+    v = op(v, dppm<0x114, 0xF, 0xF>(T(0), v));  // row_shr 4, 8: rows 0 .. 2, and row 3's steps 16 + k - 1, - 2
+    v = op(v, dppm<0x118, 0xF, 0xF>(T(0), v));
+    // a tail lane adds its plant's row total (lane 16 h + 15); row lanes read lane 63's zero
+    const int src = lane >= 48 ? 16 * (lane & 3) + 15 : 63;
+    return op(v, lane_fetch(v, 4 * src));
+}
+template <typename T, typename F> __device__ __forceinline__ T lay3_suffix(T v, F op, int lane)
+{
+    v = op(v, dppm<0x101, 0x7, 0xF>(T(0), v));  // row_shl 1, 2: rows 0 .. 2 only
+    v = op(v, dppm<0x102, 0x7, 0xF>(T(0), v));
+    v = op(v, dppm<0x104, 0xF, 0xF>(T(0), v));  // row_shl 4, 8: and row 3's steps 16 + k + 1, + 2
+    v = op(v, dppm<0x108, 0xF, 0xF>(T(0), v));
+    // a row lane adds its plant's tail suffix (step 16: lane 48 + h); tail lanes read lane 63's zero
+    const int src = lane < 48 ? 48 + (lane >> 4) : 63;
+    return op(v, lane_fetch(v, 4 * src));
+}
+// LAY 3 reduction over a plant's steps, every lane of the plant ending on the same bits (as half_reduce:
+// the row butterfly, the tail's pairs (16, 17), (18, 19) then their sum, then row total op tail total)
+template <typename T, typename F> __device__ __forceinline__ T lay3_reduce(T v, F op, int lane)
+{
+    v = op(v, dppm<0xB1, 0x7, 0xF>(T(0), v));   // quad_perm [1,0,3,2]     (rows 0 .. 2)
+    v = op(v, dppm<0x4E, 0x7, 0xF>(T(0), v));   // quad_perm [2,3,0,1]
+    v = op(v, dppm<0x141, 0x7, 0xF>(T(0), v));  // row_half_mirror
+    v = op(v, dppm<0x140, 0x7, 0xF>(T(0), v));  // row_mirror
+    T t = dppm<0x12C, 0x8, 0x5>(T(0), v);       // row 3: steps 16, 18 (banks 0, 2) take 17, 19 (row_ror 12) ...
+    t = dppm<0x124, 0x8, 0xA>(t, v);            // ... and 17, 19 (banks 1, 3) take 16, 18 (row_ror 4)
+    v = op(v, t);
+    v = op(v, dppm<0x128, 0x8, 0xF>(T(0), v));  // row 3: (16 + 17) with (18 + 19) (row_ror 8)
+    const int src = lane < 48 ? 48 + (lane >> 4) : ((lane & 3) == 3 ? 63 : 16 * (lane & 3));
+    v = op(v, lane_fetch(v, 4 * src));
+    // a lane of no plant counts in plant 2's slot: it takes plant 2's result and so decides with plant 2
+    // (its status and `done` must not hold the wave)
+    return lane_fetch(v, 4 * ((lane & 51) == 51 ? 32 : lane));
+}
+template <int LAY, typename T> __device__ __forceinline__ T l_psum(T v, int lane)
+{
+    if constexpr (LAY == 3) return lay3_prefix(v, [](T a, T b) { return a + b; }, lane);
+    else return psum(v);
+}
+template <int LAY, typename T> __device__ __forceinline__ T l_ssum(T v, int lane)
+{
+    if constexpr (LAY == 3) return lay3_suffix(v, [](T a, T b) { return a + b; }, lane);
+    else return ssum(v, lane);
+}
+template <int LAY, typename T> __device__ __forceinline__ T l_prefix_max(T v, int lane)
+{
+    if constexpr (LAY == 3) return lay3_prefix(v, [](T a, T b) { return hwmax(a, b); }, lane);
+    else return half_prefix(v, [](T a, T b) { return hwmax(a, b); });
+}
+template <int LAY, typename T> __device__ __forceinline__ T l_suffix_max(T v, int lane)
+{
+    if constexpr (LAY == 3) return lay3_suffix(v, [](T a, T b) { return hwmax(a, b); }, lane);
+    else return half_suffix(v, [](T a, T b) { return hwmax(a, b); }, lane);
+}
+// LAY 3 maximum over a plant's steps: max is exact in any order, so the tail folds into the row first (row
+// lane r < 4 takes step 16 + r by ds_bpermute), the row butterfly needs no masks (row 3 is ignored), and
+// the tail lanes read their row's result back
+template <typename T> __device__ __forceinline__ T lay3_max(T v, int lane)
+{
+    const int src_in = (lane < 48 && (lane & 15) < 4) ? 48 + 4 * (lane & 15) + (lane >> 4) : lane;
+    v = hwmax(v, lane_fetch(v, 4 * src_in));
+    v = hwmax(v, dpp_t<0xB1>(v));   // quad_perm [1,0,3,2]
+    v = hwmax(v, dpp_t<0x4E>(v));   // quad_perm [2,3,0,1]
+    v = hwmax(v, dpp_t<0x141>(v));  // row_half_mirror
+    v = hwmax(v, dpp_t<0x140>(v));  // row_mirror
+    const int src_out = lane < 48 ? lane : 16 * lay3_plant(lane);  // (a lane of no plant: plant 2's)
+    return lane_fetch(v, 4 * src_out);
+}
+template <int LAY, typename T> __device__ __forceinline__ T l_max(T v, int lane)
+{
+    if constexpr (LAY == 3) return lay3_max(v, lane);
+    else return hmax(v);
+}
+template <int LAY, typename T> __device__ __forceinline__ T l_sum(T v, int lane)
+{
+    if constexpr (LAY == 3) return lay3_reduce(v, [](T a, T b) { return a + b; }, lane);
+    else return hsum(v);
+}
+template <int LAY> __device__ __forceinline__ bool l_any(bool p, int lane)  // any lane of this lane's plant
+{
+    const unsigned long long b = __ballot(p);
+    if constexpr (LAY == 3) {
+        const int h = lay3_plant(lane);
+        return (b & ((0xFFFFull << (16 * h)) | (0x1111ull << (48 + h)))) != 0ull;
+    } else {
+        return ((lane & 32) ? (b >> 32) : (b & 0xffffffffull)) != 0ull;
+    }
+}
+
+// Per plant in LDS (fp64).  P^ is kept as its packed upper triangle (row i holds columns i .. N-1 at
+// i NC - i (i - 1) / 2): OSQP's own P, one copy of each entry.  Union region u: first the condensing
+// recurrences' histories V, Cr, then the lag table G (packed like P: G(d, T) for d + T < N), then P^ and
+// the vectors Dv .. piv, each written once what it overlaps is dead.
 template <int NC> struct PlantLds {
-    static constexpr int LD = NC + 1;  // odd row stride: column walks by lane are conflict-free
-    double Ph[NC * LD];                // scaled P^ (row r by lane r); before that the condensing scratch
-    double CAB[NC], CS[NC], Dv[NC], Ev[NC], SE[NC], qh[NC], Ut[NC], Ub[NC], piv[NC], tmp[NC];
+    static constexpr int NP = NC * (NC + 1) / 2;
+    static constexpr int NU = (NC + 1) * 16 > NP + 7 * NC ? (NC + 1) * 16 : NP + 7 * NC;
+    static_assert(NP % 2 == 0, "16-B aligned vectors");
+    double u[NU];
+    double CS[NC], tmp[NC];
     double sh[4];  // cost, 1 / cost, U, K0
+    __device__ double *V() { return u; }
+    __device__ double *Cr() { return u + (NC + 1) * 8; }
+    __device__ double *G() { return u; }
+    __device__ double *Ph() { return u; }
+    __device__ double *Dv() { return u + NP; }
+    __device__ double *Ev() { return u + NP + NC; }
+    __device__ double *SE() { return u + NP + 2 * NC; }
+    __device__ double *qh() { return u + NP + 3 * NC; }
+    __device__ double *Ut() { return u + NP + 4 * NC; }
+    __device__ double *Ub() { return u + NP + 5 * NC; }
+    __device__ double *piv() { return u + NP + 6 * NC; }
+    __device__ const double *Dv() const { return u + NP; }
+    __device__ const double *Ev() const { return u + NP + NC; }
+    __device__ const double *qh() const { return u + NP + 3 * NC; }
+    __device__ const double *Ut() const { return u + NP + 4 * NC; }
+    __device__ const double *Ub() const { return u + NP + 5 * NC; }
+    // packed upper-triangle index of (i, j), i, j < NC
+    __device__ static int pk(int i, int j)
+    {
+        const int a = i < j ? i : j, b = i < j ? j : i;
+        return a * NC - (a * (a - 1)) / 2 + (b - a);
+    }
 };
 
 // Gauss-Jordan inverse of this half's SPD matrix (n x n; SPD: no pivoting), lane r holding row r in
@@ -195,21 +357,23 @@ __device__ __forceinline__ bool gj_rows(double (&row)[NC], double *piv, int n, i
     return ok;
 }
 
-// WPE: waves per SIMD the register allocation is held to (2, or 3 for A/B: MPCQ_PLANT_WPE)
-template <typename T, int NC, int WPE>
+// WPE: waves per SIMD the register allocation is held to (2, or 3 for A/B: MPCQ_PLANT_WPE); LAY: plants per
+// wave (2: one per 32-lane half; 3: N <= 20, rows plus interleaved tails, see lay3_*)
+template <typename T, int NC, int WPE, int LAY>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? WPE : 2, NC <= 20 ? 8 : 4))) void plant_step_kernel(PlantStepArgs a)
 {
     static_assert(NC % 4 == 0, "broadcast rows are read 16 B at a time");
-    constexpr int LD = NC + 1;
-    __shared__ PlantLds<NC> lds[2];
-    __shared__ __attribute__((aligned(16))) T bx[2][NC], bw[2][NC];  // per-half broadcasts
-    const int lane = threadIdx.x, h = lane >> 5, r = lane & 31;
-    const int plant = blockIdx.x * 2 + h;
+    static_assert(LAY == 2 || (LAY == 3 && NC <= 20), "three plants per wave: N <= 20");
+    using PL = PlantLds<NC>;
+    __shared__ PL lds[LAY];
+    __shared__ __attribute__((aligned(16))) T bx[LAY][NC], bw[LAY][NC];  // per-plant broadcasts
+    const int lane = threadIdx.x, h = lay_plant<LAY>(lane), r = lay_row<LAY>(lane);
+    const int plant = blockIdx.x * LAY + h;
     const bool live = plant < a.n_plants;
     const int p = live ? plant : 0;  // a dead half runs plant 0's data and publishes nothing
     const int N = a.N, n = N, nx = a.nx;
     const bool lr = r < N;
-    PlantLds<NC> &S = lds[h];
+    PL &S = lds[h];
     T *bxh = bx[h], *bwh = bw[h];
     const SolverSettings &st = a.st;
     // cold-path views: lane indices re-derived opaquely, so the loop does not keep the addresses of
@@ -223,8 +387,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     // ---------------------------------------------------------------- 1. condensing
     // CAB[k] = Cd Ad^k Bd and c_k = Cd Ad^k (Sx row k-1) by the recurrences v_{k+1} = Ad v_k,
     // c_{k+1} = c_k Ad: lane t < nx of the half owns component t (scratch in the P^ slot).
-    double *V = S.Ph, *Cr = S.Ph + (NC + 1) * 8;  // V[k][8], Cr[k][8] for k <= N
-    static_assert((NC + 1) * 16 <= NC * LD, "condensing scratch fits the P^ slot");
+    double *V = S.V(), *Cr = S.Cr();  // V[k][8], Cr[k][8] for k <= N (the union region)
     {
         const double *Ad = a.Ad + (size_t)p * nx * nx, *Bd = a.Bd + (size_t)p * nx, *Cd = a.Cd + (size_t)p * nx;
         double adr[8], adc[8];  // row t and column t of Ad
@@ -257,7 +420,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
 #pragma unroll
             for (int s = 0; s < 8; s++) cab += Cd[s < nx ? s : 0] * (s < nx ? V[r * 8 + s] : 0.0);
         }
-        const double cs = psum(cab);  // Su(i, j) = CS[i - j] = sum_{k <= i - j} CAB[k]
+        const double cs = l_psum<LAY>(cab, lane);  // Su(i, j) = CS[i - j] = sum_{k <= i - j} CAB[k]
         if (r < NC) S.CS[r] = lr ? cs : 0.0;
         wave_sync();
     }
@@ -287,15 +450,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     // max(r, j)) with G(d, T) = sum_{t <= T} CS[t] CS[t + d]: lane t forms CS[t] CS[t + d] for every lag
     // d, one prefix scan per lag gives G(d, .) across the lanes, and lane r gathers its row from LDS
     // (the recurrences' scratch is dead by now).  Row r stays in registers.
-    double *G = S.Ph;  // G[d][t], stride LD
+    double *G = S.G();  // G(d, T) at pk(d, d + T), d + T < NC
     {
         const double ct = lr ? S.CS[r] : 0.0;
 #pragma unroll
         for (int d = 0; d < NC; d++) {
             const int td = r + d < NC ? r + d : NC - 1;
             const double prod = (lr && r + d < N) ? ct * S.CS[td] : 0.0;
-            const double g = psum(prod);
-            if (r < NC) G[d * LD + r] = g;
+            const double g = l_psum<LAY>(prod, lane);
+            if (r + d < NC) G[PL::pk(d, d + r)] = g;
         }
     }
     wave_sync();
@@ -305,13 +468,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         double v = 0.0;
         if (lr && j < N) {
             const int mx = r > j ? r : j, d = r > j ? r - j : j - r;
-            v = 2.0 * ((R * (double)(N - mx) + (r == j ? RD : 0.0)) + Q * G[d * LD + (N - 1 - mx)]);
+            v = 2.0 * ((R * (double)(N - mx) + (r == j ? RD : 0.0)) + Q * G[PL::pk(d, d + N - 1 - mx)]);
         }
         pr[j] = v;
     }
     double qk = 0.0;
     if (lr) {
-        const double Fu = 2.0 * (R + Q * G[r * LD + (N - 1 - r)]);  // Fu[r] (:305, incl. the diagonal() quirk: R 1)
+        const double Fu = 2.0 * (R + Q * G[PL::pk(r, N - 1)]);  // Fu[r] (:305, incl. the diagonal() quirk: R 1)
         double f = 0.0;
         for (int k = r; k < N; k++) f += S.CS[k - r] * (S.tmp[k] - a.xref);
         qk = (2.0 * Q) * f + Fu * Uv;
@@ -330,12 +493,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     const double aK0 = fabs(K0);
     double Dr = lr ? 1.0 : 0.0, Er = lr ? 1.0 : 0.0;  // (0 on dead lanes: neutral in every scan)
     double cost = 1.0, cp = 1.0;
-    auto dmax = [](double x, double y) { return hwmax(x, y); };
     for (int it = 0; it < st.scaling; it++) {
         double vp = 0.0;
 #pragma unroll
         for (int j = 0; j < NC; j++) vp = hwmax_abs(vp, pr[j]);
-        const double emax = half_suffix(Er, dmax, lane), dpre = half_prefix(Dr, dmax);
+        const double emax = l_suffix_max<LAY>(Er, lane), dpre = l_prefix_max<LAY>(Dr, lane);
         const double va = (aK0 * Dr) * emax, ve = (aK0 * Er) * dpre;
         const double dt = 1.0 / sqrt(limit_scaling_p(fmax(cp * vp, va)));
         const double et = 1.0 / sqrt(limit_scaling_p(ve));
@@ -351,7 +513,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         }
         wave_sync();
         if (lr) { Dr *= dt; Er *= et; }
-        const double mean = hsum(lr ? cn : 0.0) / n;
+        const double mean = l_sum<LAY>(lr ? cn : 0.0, lane) / n;
         cp = 1.0 / limit_scaling_p(fmax(mean, 1.0));
         cost *= cp;
     }
@@ -360,15 +522,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         for (int j = 0; j < NC; j++) pr[j] *= cp;
     }
     const double cinv = 1.0 / cost;
-    if (r < NC) {
+    if (r < NC) {  // (the lag table under P^ is dead: the rows are in registers)
 #pragma unroll
-        for (int j = 0; j < NC; j++) S.Ph[r * LD + j] = pr[j];  // (zero rows beyond N)
-        S.Dv[r] = Dr;
-        S.Ev[r] = Er;
+        for (int j = 0; j < NC; j++)
+            if (j >= r) S.Ph()[PL::pk(r, j)] = pr[j];  // the upper triangle, row r by lane r (zero rows beyond N)
+        S.Dv()[r] = Dr;
+        S.Ev()[r] = Er;
     }
     {
-        const double se = ssum(Er * Er, lane);  // sum_{i >= r} E_i^2: A^'A^ = 2 K0^2 D_r D_k SE[max(r, k)]
-        if (r < NC) S.SE[r] = se;
+        const double se = l_ssum<LAY>(Er * Er, lane);  // sum_{i >= r} E_i^2: A^'A^ = 2 K0^2 D_r D_k SE[max(r, k)]
+        if (r < NC) S.SE()[r] = se;
     }
 
     // ---------------------------------------------------------------- 3. controllerStep front end
@@ -385,9 +548,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     }
     if (r < NC) {  // the values only the checks and the finalize read stay in LDS (read there, after
                    // the loop's wave_syncs: not hoisted into registers for the whole solve)
-        S.qh[r] = (double)qh;  // q^ as the iteration sees it
-        S.Ut[r] = up_t;
-        S.Ub[r] = up_b;
+        S.qh()[r] = (double)qh;  // q^ as the iteration sees it
+        S.Ut()[r] = up_t;
+        S.Ub()[r] = up_b;
     }
     if (r == 0) {
         S.sh[0] = cost;
@@ -397,8 +560,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     }
     // the update's checks (l^ = -DBL_MAX E stays free of -OSQP_INFTY MIN_SCALING): u < l cannot occur;
     // a row whose u^ reaches OSQP_INFTY MIN_SCALING would change type (TYPE_CHANGED)
-    int status = hany(lr && ((double)ut > kInfty * kMinScaling || (double)ub > kInfty * kMinScaling)) ? kTypeChanged
-                                                                                                     : kUnsolved;
+    int status = l_any<LAY>(lr && ((double)ut > kInfty * kMinScaling || (double)ub > kInfty * kMinScaling), lane)
+                     ? kTypeChanged
+                     : kUnsolved;
 
     // ---------------------------------------------------------------- 4. ADMM
     // M(rho) = P^ + sigma I + rho A^'A^ (set_rho_vec: every row an inequality at rho) and its inverse
@@ -415,25 +579,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     T gk = T(0);
     const double Dd = lr ? Dr : 0.0, A2 = 2.0 * K0 * K0;
     auto factor = [&](double rho) -> bool {
-        const int cl = cold_lane(), r = cl & 31;
-        PlantLds<NC> &S = lds[cl >> 5];
+        const int cl = cold_lane(), r = lay_row<LAY>(cl);
+        PL &S = lds[lay_plant<LAY>(cl)];
         double row[NC];
 #pragma unroll
         for (int j = 0; j < NC; j++) {
             double v = 0.0;
             if (lr && j < n) {
                 const int mx = r > j ? r : j;
-                v = S.Ph[r * LD + j] + (r == j ? st.sigma : 0.0) + rho * (((A2 * Dd) * S.Dv[j]) * S.SE[mx]);
+                v = S.Ph()[PL::pk(r, j)] + (r == j ? st.sigma : 0.0) + rho * (((A2 * Dd) * S.Dv()[j]) * S.SE()[mx]);
             }
             row[j] = v;
         }
-        const bool ok = gj_rows<NC>(row, S.piv, n, r);
+        const bool ok = gj_rows<NC>(row, S.piv(), n, r);
         double g = 0.0, pre = 0.0;
 #pragma unroll
         for (int j = 0; j < NC; j += 2) {
-            const double2 q2 = *(const double2 *)(S.qh + j);
-            const double2 d2 = *(const double2 *)(S.Dv + j);
-            const double2 e2 = *(const double2 *)(S.Ev + j);
+            const double2 q2 = *(const double2 *)(S.qh() + j);
+            const double2 d2 = *(const double2 *)(S.Dv() + j);
+            const double2 e2 = *(const double2 *)(S.Ev() + j);
             g = fma(row[j], q2.x, g);
             g = fma(row[j + 1], q2.y, g);
             if constexpr (MERGED) {
@@ -471,13 +635,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     bool done = false, setup_ok = true, first = true, refactor = true;
 
     auto finalize = [&]() {
-        const int cl = cold_lane(), r = cl & 31;
-        const PlantLds<NC> &S = lds[cl >> 5];
-        const int plant = blockIdx.x * 2 + (cl >> 5);
+        const int cl = cold_lane(), r = lay_row<LAY>(cl);
+        const PL &S = lds[lay_plant<LAY>(cl)];
+        const int plant = blockIdx.x * LAY + lay_plant<LAY>(cl);
         const bool has_sol = status == kSolved || status == kSolvedInaccurate || status == kMaxIterReached;
         if (!live) return;
         if (lr) {
-            const double Er = S.Ev[r], Dr = S.Dv[r], cinv = S.sh[1], Uv = S.sh[2];
+            const double Er = S.Ev()[r], Dr = S.Dv()[r], cinv = S.sh[1], Uv = S.sh[2];
             const double xv = has_sol ? (double)xs * Dr : __builtin_nan("");
             a.x[(size_t)plant * n + r] = xv;
             if (r == 0) {
@@ -492,14 +656,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     };
     // P^ v for this half (row r of P^ from LDS, v broadcast)
     auto p_times = [&](T v) -> double {
-        const int cl = cold_lane(), r = cl & 31;
-        PlantLds<NC> &S = lds[cl >> 5];
-        T *bxh = bx[cl >> 5];
+        const int cl = cold_lane(), r = lay_row<LAY>(cl);
+        PL &S = lds[lay_plant<LAY>(cl)];
+        T *bxh = bx[lay_plant<LAY>(cl)];
         if (r < NC) bxh[r] = lr ? v : T(0);
         wave_sync();
         double acc = 0.0;
         if (lr)
-            for (int i = 0; i < n; i++) acc = fma(S.Ph[r * LD + i], (double)bxh[i], acc);
+            for (int i = 0; i < n; i++) acc = fma(S.Ph()[PL::pk(r, i)], (double)bxh[i], acc);
         wave_sync();
         return acc;
     };
@@ -530,7 +694,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         const T wt = tt_fma(rho, zt, -yt) - tt_fma(rho, zb, -yb);
         T xi;
         if constexpr (MERGED) {
-            const T atw = (DT * K0T) * ssum(ET * wt, lane);  // A^'(w_top - w_bot)
+            const T atw = (DT * K0T) * l_ssum<LAY>(ET * wt, lane);  // A^'(w_top - w_bot)
             if (r < NC) bxh[r] = lr ? tt_fma(sigT, xs, atw) : T(0);
             wave_sync();
             xi = row_dot(Srow, bxh, gk);
@@ -550,7 +714,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         // z~ = A^ x~ (top rows; bottom = -top), relaxation, projection onto [l, u], dual update
         T ETl = ET;
         asm volatile("" : "+v"(ETl));
-        const T zz = (ETl * K0T) * psum(DT * xi);
+        const T zz = (ETl * K0T) * l_psum<LAY>(DT * xi, lane);
         T dyt = T(0), dyb = T(0);
         if (lr && !done) {
             T v = tt_fma(alpha, zz, oma * zt);
@@ -570,17 +734,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         // iterate (exact in fp64), so an fp32 kernel takes OSQP's decisions on the same numbers as an
         // fp64 one does on its own iterate (half-wave reductions)
         using TD = double;
-        const int cl = cold_lane(), rc = cl & 31;
-        const PlantLds<NC> &C = lds[cl >> 5];
-        const TD Erl = lr ? C.Ev[rc] : 1.0, Drl = lr ? C.Dv[rc] : 1.0, Ddl = lr ? Drl : 0.0, qsl = lr ? C.qh[rc] : 0.0;
-        const TD utl = lr ? C.Ut[rc] : 0.0, ubl = lr ? C.Ub[rc] : 0.0;
+        const int cl = cold_lane(), rc = lay_row<LAY>(cl);
+        const PL &C = lds[lay_plant<LAY>(cl)];
+        const TD Erl = lr ? C.Ev()[rc] : 1.0, Drl = lr ? C.Dv()[rc] : 1.0, Ddl = lr ? Drl : 0.0, qsl = lr ? C.qh()[rc] : 0.0;
+        const TD utl = lr ? C.Ut()[rc] : 0.0, ubl = lr ? C.Ub()[rc] : 0.0;
         const TD costl = C.sh[0], cinvl = C.sh[1], K0l = C.sh[3];
         const TD xd = (TD)xs, ztd = (TD)zt, zbd = (TD)zb, ytd = (TD)yt, ybd = (TD)yb, dxd = (TD)dx;
         const TD EKd = lr ? Erl * K0l : 0.0, DKd = Ddl * K0l, Ed = lr ? Erl : 0.0;
         const TD EiD = 1.0 / Erl, DiD = 1.0 / Drl;
         const TD utd = lr ? utl * Erl : 0.0, ubd = lr ? ubl * Erl : 0.0;  // (== (T) bounds for fp64)
-        const TD ax = EKd * psum(Ddl * xd);
-        const TD aty = DKd * ssum(Ed * (ytd - ybd), lane);
+        const TD ax = EKd * l_psum<LAY>(Ddl * xd, lane);
+        const TD aty = DKd * l_ssum<LAY>(Ed * (ytd - ybd), lane);
         const TD px = p_times(xs);
         TD ax_z = 0, ax_zs = 0, zn_s = 0, zn_r = 0, axn_s = 0, axn_r = 0;
         TD dr_r = 0, dr_s = 0, qn_r = 0, qn_s = 0, atyn_r = 0, atyn_s = 0, pxn_r = 0, pxn_s = 0;
@@ -602,10 +766,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
             pxn_r = fabs(px);
             pxn_s = fabs(DiD * px);
         }
-        ax_z = hmax(ax_z); ax_zs = hmax(ax_zs); zn_s = hmax(zn_s); zn_r = hmax(zn_r);
-        axn_s = hmax(axn_s); axn_r = hmax(axn_r);
-        dr_r = hmax(dr_r); dr_s = hmax(dr_s); qn_r = hmax(qn_r); qn_s = hmax(qn_s);
-        atyn_r = hmax(atyn_r); atyn_s = hmax(atyn_s); pxn_r = hmax(pxn_r); pxn_s = hmax(pxn_s);
+        auto pmax = [&](TD v) { return l_max<LAY>(v, lane); };
+        ax_z = pmax(ax_z); ax_zs = pmax(ax_zs); zn_s = pmax(zn_s); zn_r = pmax(zn_r);
+        axn_s = pmax(axn_s); axn_r = pmax(axn_r);
+        dr_r = pmax(dr_r); dr_s = pmax(dr_s); qn_r = pmax(qn_r); qn_s = pmax(qn_s);
+        atyn_r = pmax(atyn_r); atyn_s = pmax(atyn_s); pxn_r = pmax(pxn_r); pxn_s = pmax(pxn_s);
         const TD pri_res = scaled_term ? ax_z : ax_zs;
         const TD dua_res = scaled_term ? dr_r : cinvl * dr_s;
 
@@ -615,27 +780,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
             const TD d1 = fmax((TD)dyt, 0.0), d2 = fmax((TD)dyb, 0.0);
             TD ndy = lr ? fmax(fabs(scaled_term ? d1 : Erl * d1), fabs(scaled_term ? d2 : Erl * d2)) : 0.0;
             TD lhs = lr ? utd * d1 + ubd * d2 : 0.0;
-            ndy = hmax(ndy);
-            lhs = hsum(lhs);
+            ndy = pmax(ndy);
+            lhs = l_sum<LAY>(lhs, lane);
             const bool cand = ndy > kDivisionTol && lhs < eps * ndy;
             if (!wave_any(cand)) return false;
-            const TD atd = DKd * ssum(Ed * (d1 - d2), lane);
-            const TD nat = hmax(lr ? fabs(scaled_term ? atd : DiD * atd) : 0.0);
+            const TD atd = DKd * l_ssum<LAY>(Ed * (d1 - d2), lane);
+            const TD nat = pmax(lr ? fabs(scaled_term ? atd : DiD * atd) : 0.0);
             return cand && nat < eps * ndy;
         };
         // OSQP is_dual_infeasible on delta_x; the P^ dx and A^ dx products only when some half is a
         // candidate
         auto dual_infeasible = [&](TD eps) -> bool {
-            const TD qdx = hsum(lr ? qsl * dxd : 0.0);
-            const TD ndx = hmax(lr ? fabs(scaled_term ? dxd : Drl * dxd) : 0.0);
+            const TD qdx = l_sum<LAY>(lr ? qsl * dxd : 0.0, lane);
+            const TD ndx = pmax(lr ? fabs(scaled_term ? dxd : Drl * dxd) : 0.0);
             const TD cs = scaled_term ? 1.0 : costl;
             const bool cand = ndx > kDivisionTol && qdx < -cs * eps * ndx;
             if (!wave_any(cand)) return false;
             const TD t2 = p_times(dx);
-            const TD t3 = EKd * psum(Ddl * dxd);
-            const TD npdx = hmax(lr ? fabs(scaled_term ? t2 : DiD * t2) : 0.0);
+            const TD t3 = EKd * l_psum<LAY>(Ddl * dxd, lane);
+            const TD npdx = pmax(lr ? fabs(scaled_term ? t2 : DiD * t2) : 0.0);
             const TD sv = scaled_term ? t3 : EiD * t3;
-            const bool viol = hany(lr && (sv > eps * ndx || -sv > eps * ndx));  // rows r (u finite), N + r (-A x)
+            const bool viol = l_any<LAY>(lr && (sv > eps * ndx || -sv > eps * ndx), lane);  // rows r (u finite), N + r (-A x)
             return cand && npdx < cs * eps * ndx && !viol;
         };
         auto check_termination = [&](bool approx) -> int {
@@ -694,13 +859,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     if (threadIdx.x == 0 && !wave_all(setup_ok || !live)) atomicOr(a.flags, 1);
 }
 
+template <typename T, int NC, int LAY>
+int plant_step_launch_l(const PlantStepArgs &a, hipStream_t s)
+{
+    const dim3 grid((a.n_plants + LAY - 1) / LAY), block(64);
+    if (NC <= 20 && a.wpe == 3) hipLaunchKernelGGL((plant_step_kernel<T, NC, 3, LAY>), grid, block, 0, s, a);
+    else if (NC <= 20 && a.wpe == 4) hipLaunchKernelGGL((plant_step_kernel<T, NC, 4, LAY>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((plant_step_kernel<T, NC, 2, LAY>), grid, block, 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+// N in 17 .. 20: three plants per wave unless PlantStepArgs::layout asks for two (test hook)
 template <typename T, int NC>
 int plant_step_launch_t(const PlantStepArgs &a, hipStream_t s)
 {
-    if (NC <= 20 && a.wpe == 3) hipLaunchKernelGGL((plant_step_kernel<T, NC, 3>), dim3((a.n_plants + 1) / 2), dim3(64), 0, s, a);
-    else if (NC <= 20 && a.wpe == 4) hipLaunchKernelGGL((plant_step_kernel<T, NC, 4>), dim3((a.n_plants + 1) / 2), dim3(64), 0, s, a);
-    else hipLaunchKernelGGL((plant_step_kernel<T, NC, 2>), dim3((a.n_plants + 1) / 2), dim3(64), 0, s, a);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
+    if constexpr (NC == 20) {
+        if (a.layout != 2) return plant_step_launch_l<T, NC, 3>(a, s);
+    }
+    return plant_step_launch_l<T, NC, 2>(a, s);
 }
 
 }  // namespace mpcq

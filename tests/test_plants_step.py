@@ -76,6 +76,32 @@ def test_fp32_matches_oracle(plant):
 
 
 @pytest.mark.parametrize("dtype", ["f32", "f64"])
+@pytest.mark.parametrize("N,B", [(20, 301), (17, 98)])
+def test_three_plants_per_wave_match_two(plant, dtype, N, B, monkeypatch):
+    """At 17 <= N <= 20 the kernel runs three plants per wave (rows plus interleaved tails, lay3_* in
+    mpcq_plant.hip) with the association of the two-plants-per-wave layout: every output bit for bit the
+    same as MPCQ_PLANT_LAYOUT=2, and each plant's result independent of its slot (0, 1, 2) in the wave."""
+    Ad, Bd, X, U = _plants(plant, B, 3)
+    out = {}
+    for lay in ("2", None):
+        if lay:
+            monkeypatch.setenv("MPCQ_PLANT_LAYOUT", lay)
+        else:
+            monkeypatch.delenv("MPCQ_PLANT_LAYOUT", raising=False)
+        s, Ug = _fused(plant, Ad, Bd, X, U, N, dtype)
+        out[lay] = (s.solution(), s.dual(), Ug, *s.info())
+        s.close()
+    for a_, b_ in zip(out["2"], out[None]):
+        assert np.array_equal(a_, b_, equal_nan=True)
+    # the same plants shifted by one slot (a leading copy of plant 0): identical results
+    sh = lambda v: np.concatenate([v[:1], v])  # noqa: E731
+    s, Ug = _fused(plant, sh(Ad), sh(Bd), sh(X), sh(U), N, dtype)
+    assert np.array_equal(s.solution()[1:], out[None][0]) and np.array_equal(Ug[1:], out[None][2])
+    assert np.array_equal(s.info()[1][1:], out[None][4])
+    s.close()
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
 def test_plant_result_independent_of_wave_partner(plant, dtype):
     """Two plants share a wave (one per 32-lane half) and a refactorisation is wave-uniform: a plant
     whose rho never moves must give the same bits whether its partner half adapts rho or not
