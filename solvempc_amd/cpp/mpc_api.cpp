@@ -47,18 +47,28 @@ ModelPredictiveControlAPI::ModelPredictiveControlAPI(bool verbose_, const std::s
     U = Matrix::Zero(N_O, N_O);
     t0 = dt = 0.0;
 
-    setSystemVars();
-    setCosts();
-    setLiftedCosts();
-    setTransformations();
-    setLL();
-    setH();
-    setLu();
-    setFVars();
-    setLinearConstraints();
-    setUpperBound();
-    updateRef(xref);
-    setF();
+    // The condensing runs on the device (condense_on_device).  A host without a usable MI355X fails here:
+    // that is this drop-in's counterpart of the reference's solver failure, so it takes the same exit,
+    // solverFlag = false (the caller's `if(!mpc.solverFlag){return 1;}`, solver.cpp:28), with the
+    // library's reason on stderr, instead of an exception the reference's caller does not catch.
+    try {
+        setSystemVars();
+        setCosts();
+        setLiftedCosts();
+        setTransformations();
+        setLL();
+        setH();
+        setLu();
+        setFVars();
+        setLinearConstraints();
+        setUpperBound();
+        updateRef(xref);
+        setF();
+    } catch (const DeviceError &e) {
+        std::cerr << e.what() << std::endl;
+        solverFlag = false;
+        return;
+    }
 
     lb = Matrix(2 * horizon, 1, -DBL_MAX);  // :42
     ub = Matrix(2 * horizon, 1);            // :43  W0 + Sbar X + Ku U
@@ -145,7 +155,7 @@ void ModelPredictiveControlAPI::condense_on_device()
     const double q = Q(0, 0), r = R(0, 0), rd = RD(0, 0);
     if (mpcq_condense(device_, 1, N_S, N, 10, ad.data(), bd.data(), cd.data(), k.data(), &q, &r, &rd, P.data(),
                       A.data(), fx.data(), fu.data(), fr.data(), sbar.data(), ku.data(), w0.data()) != MPCQ_OK)
-        throw std::runtime_error(std::string("[MPC API]\tcondensing failed: ") + mpcq_last_error());
+        throw DeviceError(std::string("[MPC API]\tcondensing failed: ") + mpcq_last_error());
     H = Matrix::from_row_major(N, N, P.data());
     Gbar = Matrix::from_row_major(2 * N, N, A.data());
     Fx = Matrix::from_row_major(N, N_S, fx.data());

@@ -10,6 +10,7 @@
 // mpcq::Solver (osqp-eigen surface over the C ABI).
 #pragma once
 
+#include <stdexcept>
 #include <string>
 
 #include "json_lite.hpp"
@@ -19,6 +20,12 @@ constexpr int mpcWindow = 15;  // default horizon (reference: compile-time const
 constexpr int N_S = 4;         // states
 constexpr int N_C = 1;         // controls
 constexpr int N_O = 1;         // outputs
+
+// A device-side build step of the constructor failed (no usable device): the constructor reports it and
+// leaves solverFlag false, the reference's failure exit.
+struct DeviceError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
 
 class ModelPredictiveControlAPI {
 public:

@@ -117,3 +117,16 @@ def test_cli_missing_config_is_a_parse_error(tmp_path):
                        timeout=60)
     assert r.returncode != 0
     assert "json.exception.parse_error.101" in r.stderr
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a host with a GPU driver: the device path runs")
+def test_cli_without_device_takes_the_solver_flag_exit():
+    """BASELINE config 1 on a host with no device: the drop-in's constructor, whose
+    condensing runs on the device, reports the failure and leaves solverFlag false, so the CLI takes the
+    reference's own exit (`if(!mpc.solverFlag){return 1;}`, solver.cpp:28) instead of aborting."""
+    exe = ROOT / "solvempc_amd" / "solvempc"
+    r = subprocess.run([str(exe), "-c", str(ROOT / "tests" / "golden" / "plant_mpc_api.json")], input="",
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1, (r.returncode, r.stderr)
+    assert "condensing failed" in r.stderr
+    assert "Entering control loop" not in r.stdout
