@@ -318,6 +318,10 @@ template <int NC> struct PlantLds {
         const int a = i < j ? i : j, b = i < j ? j : i;
         return a * NC - (a * (a - 1)) / 2 + (b - a);
     }
+    // the same for row r's element i with q = row_q(r): an unrolled walk over i then costs one select per
+    // element (both forms are a register plus a constant)
+    __device__ static int row_q(int r) { return r * NC - (r * (r - 1)) / 2 - r; }
+    __device__ static int pk_row(int r, int i, int q) { return i < r ? i * NC - (i * (i - 1)) / 2 - i + r : q + i; }
 };
 
 // Gauss-Jordan inverse of this half's SPD matrix (n x n; SPD: no pivoting), lane r holding row r in
@@ -582,12 +586,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         const int cl = cold_lane(), r = lay_row<LAY>(cl);
         PL &S = lds[lay_plant<LAY>(cl)];
         double row[NC];
+        const int q = PL::row_q(r);
 #pragma unroll
         for (int j = 0; j < NC; j++) {
             double v = 0.0;
             if (lr && j < n) {
                 const int mx = r > j ? r : j;
-                v = S.Ph()[PL::pk(r, j)] + (r == j ? st.sigma : 0.0) + rho * (((A2 * Dd) * S.Dv()[j]) * S.SE()[mx]);
+                v = S.Ph()[PL::pk_row(r, j, q)] + (r == j ? st.sigma : 0.0) + rho * (((A2 * Dd) * S.Dv()[j]) * S.SE()[mx]);
             }
             row[j] = v;
         }
@@ -662,8 +667,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         if (r < NC) bxh[r] = lr ? v : T(0);
         wave_sync();
         double acc = 0.0;
-        if (lr)
-            for (int i = 0; i < n; i++) acc = fma(S.Ph()[PL::pk(r, i)], (double)bxh[i], acc);
+        if (lr) {
+            const int q = PL::row_q(r);
+#pragma unroll
+            for (int i = 0; i < NC; i++)
+                if (i < n) acc = fma(S.Ph()[PL::pk_row(r, i, q)], (double)bxh[i], acc);
+        }
         wave_sync();
         return acc;
     };
