@@ -5,7 +5,7 @@ Sums each counter over the dispatches of every kernel whose name contains one of
 divides by the number of bench steps the run made (warmup + steps), and writes
 profiles/pmc_traffic_<name>.json for bench.py's roofline.traffic.  FETCH_SIZE is doubled (MI355X_MICROARCH.md
 HBM: on gfx950 it reports half the bytes of wide coalesced reads); WRITE_SIZE is taken as reported (its
-calibration on the finalize's store shapes: tools/calib/write_calib.hip, profiles/r05_write_size_calibration.json).
+calibration on the finalize's store shapes: tools/calib/write_calib.hip, profiles/r05e_calib_write.csv).
 usage: python tools/pmc_traffic.py <pmc dir> <name> <steps> <batch> <horizon> <kernel substring>[,<substring>..]"""
 import csv
 import glob
