@@ -372,11 +372,15 @@ __global__ __launch_bounds__(kMimoSetupThreads, 8) void mimo_setup_kernel(MimoSe
         if (cj < n) {
             double m0 = 0.0, m1 = 0.0;
             const int i0 = sc * 16;
+            // packed index of (i, cj) walked down the column: +(n - i - 1) above the diagonal, +1 below
+            int idx = pk(i0, cj, n);
 #pragma unroll
             for (int ii = 0; ii < 16; ii += 2) {
                 const int i = i0 + ii;
-                if (i < n) m0 = fmax(m0, Dv[i] * fabs(P[pk(i, cj, n)]));
-                if (i + 1 < n) m1 = fmax(m1, Dv[i + 1] * fabs(P[pk(i + 1, cj, n)]));
+                const int idx1 = idx + (i < cj ? n - i - 1 : 1);
+                if (i < n) m0 = fmax(m0, Dv[i] * fabs(P[idx]));
+                if (i + 1 < n) m1 = fmax(m1, Dv[i + 1] * fabs(P[idx1]));
+                idx = idx1 + (i + 1 < cj ? n - i - 2 : 1);
             }
             cm[sc * 128 + cj] = fmax(m0, m1);
         }
