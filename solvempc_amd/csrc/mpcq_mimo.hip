@@ -143,6 +143,30 @@ __device__ __forceinline__ double dot12(const double *a, int sa, const double *b
     return s0 + s1;
 }
 
+// One 16 x 16 tile (ti, tj) of C = A B with K <= 12 on v_mfma_f64_16x16x4f64, the operands read from LDS
+// through index functors (entries outside M x K, K x N read as 0) and the valid outputs handed to `put`.
+// The whole wave runs it.  Operand layouts as in the Fx product below: lane (g = lane >> 4, c = lane & 15)
+// holds A(16 ti + c, 4 ks + g) and B(4 ks + g, 16 tj + c); accumulator v is C(16 ti + g + 4 v, 16 tj + c).
+template <typename FA, typename FB, typename FC>
+__device__ __forceinline__ void lds_mma_tile(int lane, int ti, int tj, int M, int N, int K, FA a_at, FB b_at, FC put)
+{
+    typedef double v4d __attribute__((ext_vector_type(4)));
+    v4d acc = {0.0, 0.0, 0.0, 0.0};
+    const int c = lane & 15, g = lane >> 4, m = 16 * ti + c, nn = 16 * tj + c;
+#pragma unroll
+    for (int ks = 0; ks < 3; ks++) {
+        const int k = 4 * ks + g;
+        const double av = (m < M && k < K) ? a_at(m, k) : 0.0;
+        const double bv = (nn < N && k < K) ? b_at(k, nn) : 0.0;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int v = 0; v < 4; v++) {
+        const int mm = 16 * ti + g + 4 * v;
+        if (mm < M && nn < N) put(mm, nn, acc[v]);
+    }
+}
+
 __global__ __launch_bounds__(kMimoSetupThreads, 8) void mimo_setup_kernel(MimoSetupArgs a)
 {
     extern __shared__ double sm[];
@@ -200,6 +224,10 @@ __global__ __launch_bounds__(kMimoSetupThreads, 8) void mimo_setup_kernel(MimoSe
     // one round behind (QCA_0 = QC Ad, QCA_1 = QC Ad^2 need QC: round 1)
     for (int e = t; e < ayx; e += T) QC[e] = dot12(Q + (e / nx) * ny, 1, Cd + e % nx, nx, ny);
     for (int e = t; e < anu; e += T) ABh[e] = Bd[e];
+    // each round's products as 16 x 16 MFMA tiles, one wave per tile (Ad^(2h): one tile; the AB steps: the
+    // columns of [AB_0 .. AB_(nab-1)] in tiles of 16; the QCA steps: the rows of [QCA_0; ..] in tiles of 16)
+    const int lane = t & 63, wv = t >> 6;
+    constexpr int NW = T / 64;
     for (int r = 0; r <= 5; r++) {
         __syncthreads();
         const int h = 1 << r;                          // AB: steps [h, 2h) from [0, h)
@@ -208,31 +236,38 @@ __global__ __launch_bounds__(kMimoSetupThreads, 8) void mimo_setup_kernel(MimoSe
         // QCA: round 1 forms steps 0, 1 from QC; round r >= 2 steps [2^(r-1), 2^r) from [0, 2^(r-1))
         const int hq = r >= 2 ? 1 << (r - 1) : 0;
         const int nqa = r == 1 ? (N < 2 ? N : 2) : (r >= 2 && N > hq ? (N - hq < hq ? N - hq : hq) : 0);
-        const int npw = (r < 4 && ((2 << r) < N || r == 0)) ? ann : 0;  // Ad^(2h): needed while 2h < N (Ad^2: QCA_1)
-        const int items = npw + nab * anu + nqa * ayx;
-        for (int it = t; it < items; it += T) {
-            if (it < npw) {
-                const int i = it / nx, c = it % nx;
-                Pw[r * ann + it] = dot12(Ph + i * nx, 1, Ph + c, nx, nx);
-            } else if (it < npw + nab * anu) {
-                const int f = it - npw, sdx = f / anu, e = f % anu, i = e / nu, c = e % nu;
-                ABh[(size_t)(h + sdx) * anu + e] = dot12(Ph + i * nx, 1, ABh + (size_t)sdx * anu + c, nu, nx);
-            } else {
-                const int f = it - npw - nab * anu, sdx = f / ayx, e = f % ayx, i = e / nx, c = e % nx;
-                if (r == 1) {  // QCA_0 = QC Ad, QCA_1 = QC Ad^2
-                    QCAh[(size_t)sdx * ayx + e] = dot12(QC + i * nx, 1, (sdx ? Pw : Ad) + c, nx, nx);
-                } else {       // QCA_(hq + sdx) = QCA_sdx Ad^hq (Ad^hq = Pw slot r - 2)
-                    QCAh[(size_t)(hq + sdx) * ayx + e] =
-                        dot12(QCAh + (size_t)sdx * ayx + i * nx, 1, Pw + (r - 2) * ann + c, nx, nx);
-                }
+        const int ta = (r < 4 && ((2 << r) < N || r == 0)) ? 1 : 0;  // Ad^(2h): needed while 2h < N (Ad^2: QCA_1)
+        const int tb = (nab * nu + 15) / 16;
+        const int tc = r == 1 ? nqa : (nqa * ny + 15) / 16;
+        for (int tile = wv; tile < ta + tb + tc; tile += NW) {  // (wave-uniform)
+            if (tile < ta) {
+                lds_mma_tile(lane, 0, 0, nx, nx, nx, [&](int i, int k) { return Ph[i * nx + k]; },
+                             [&](int k, int c) { return Ph[k * nx + c]; },
+                             [&](int i, int c, double v) { Pw[r * ann + i * nx + c] = v; });
+            } else if (tile < ta + tb) {  // AB_(h + s) = Ad^h AB_s, column (s, c) of the stacked AB
+                lds_mma_tile(lane, 0, tile - ta, nx, nab * nu, nx, [&](int i, int k) { return Ph[i * nx + k]; },
+                             [&](int k, int col) { return ABh[(size_t)(col / nu) * anu + k * nu + col % nu]; },
+                             [&](int i, int col, double v) { ABh[(size_t)(h + col / nu) * anu + i * nu + col % nu] = v; });
+            } else if (r == 1) {          // QCA_0 = QC Ad, QCA_1 = QC Ad^2
+                const int sdx = tile - ta - tb;
+                const double *B = sdx ? Pw : Ad;
+                lds_mma_tile(lane, 0, 0, ny, nx, nx, [&](int i, int k) { return QC[i * nx + k]; },
+                             [&](int k, int c) { return B[k * nx + c]; },
+                             [&](int i, int c, double v) { QCAh[(size_t)sdx * ayx + i * nx + c] = v; });
+            } else {                      // QCA_(hq + s) = QCA_s Ad^hq (Ad^hq = Pw slot r - 2), row (s, i)
+                const double *B = Pw + (r - 2) * ann;
+                lds_mma_tile(lane, tile - ta - tb, 0, nqa * ny, nx, nx,
+                             [&](int row, int k) { return QCAh[(size_t)(row / ny) * ayx + (row % ny) * nx + k]; },
+                             [&](int k, int c) { return B[k * nx + c]; },
+                             [&](int row, int c, double v) { QCAh[(size_t)(hq + row / ny) * ayx + (row % ny) * nx + c] = v; });
             }
         }
     }
     __syncthreads();
-    for (int it = t; it < N * ny * nu; it += T) {  // Cd Ad^d Bd
-        const int d = it / (ny * nu), i = (it / nu) % ny, c = it % nu;
-        CS[it] = dot12(Cd + i * nx, 1, ABh + (size_t)d * nx * nu + c, nu, nx);
-    }
+    for (int tile = wv; tile < (N * nu + 15) / 16; tile += NW)  // CS_d = Cd Ad^d Bd: Cd [AB_0 .. AB_(N-1)]
+        lds_mma_tile(lane, 0, tile, ny, N * nu, nx, [&](int i, int k) { return Cd[i * nx + k]; },
+                     [&](int k, int col) { return ABh[(size_t)(col / nu) * anu + k * nu + col % nu]; },
+                     [&](int i, int col, double v) { CS[(size_t)(col / nu) * ny * nu + i * nu + col % nu] = v; });
     __syncthreads();
     for (int e = t; e < ny * nu; e += T) {  // prefix over the horizon
         double acc = 0.0;
