@@ -704,7 +704,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         T xi;
         if constexpr (MERGED) {
             const T atw = (DT * K0T) * l_ssum<LAY>(ET * wt, lane);  // A^'(w_top - w_bot)
-            if (r < NC) bxh[r] = lr ? tt_fma(sigT, xs, atw) : T(0);
+            if (r < NC) bxh[r] = tt_fma(sigT, xs, atw);  // (0 on a row beyond N: x = 0, D = 0)
             wave_sync();
             xi = row_dot(Srow, bxh, gk);
             wave_sync();
@@ -717,15 +717,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
             xi = row_dot(Srow, bxh, gk) + row_dot(Btc, bwh, T(0));
             wave_sync();
         }
-        const T xn = lr ? tt_fma(alpha, xi, oma * xs) : T(0);
+        const T xn = tt_fma(alpha, xi, oma * xs);  // (0 on a row beyond N: zero M^-1 row, g = 0)
         const T dx = xn - xs;
-        if (!done) xs = xn;
+        // (no freeze of a finished plant: its results are published, its further iterates stay in its own
+        // lanes and feed nothing but its own ignored checks; a lane of no step keeps 0: zero M^-1 row,
+        // E = D = 0, u^ = OSQP_INFTY)
+        xs = xn;
         // z~ = A^ x~ (top rows; bottom = -top), relaxation, projection onto [l, u], dual update
         T ETl = ET;
         asm volatile("" : "+v"(ETl));
         const T zz = (ETl * K0T) * l_psum<LAY>(DT * xi, lane);
-        T dyt = T(0), dyb = T(0);
-        if (lr && !done) {
+        T dyt, dyb;
+        {
             T v = tt_fma(alpha, zz, oma * zt);
             T zn = tt_fmin(tt_fma(rinv, yt, v), ut);
             dyt = rho * (v - zn);
