@@ -3,8 +3,9 @@
  *
  * LukeSchmitt96/solveMPC includes "OsqpEigen/OsqpEigen.h" (include/ModelPredictiveControlAPI.h:11) and
  * owns one `OsqpEigen::Solver solver` (:144).  With this directory on the include path ahead of the
- * real osqp-eigen, that member runs its QP on a gfx950 device through include/mpcq.h and the
- * reference's calls compile unchanged:
+ * real osqp-eigen, that member runs its QP on a gfx950 device through include/mpcq.h, and the
+ * reference's call shapes below compile against it (shown by tests/cpp/reference_caller.cpp; the
+ * reference file itself also needs Eigen's unsupported MatrixFunctions, absent here: DESIGN.md section 7):
  *
  *   solver.settings()->setVerbosity(verbose); solver.settings()->setWarmStart(true);   (cpp:51-52)
  *   solver.data()->setNumberOfVariables(n); ...->setNumberOfConstraints(m);           (cpp:54-55)
