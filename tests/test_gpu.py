@@ -1196,6 +1196,49 @@ def _order_bin(v):
     return out
 
 
+@pytest.mark.parametrize("dtype", ["f64", "mixed"])
+def test_ordered_step_ragged_batch_and_snapshot(plant, dtype, monkeypatch):
+    """A ragged tile batch (10,001 QPs: a partial last wave, a partial last ordering workgroup) through the
+    hardest-first step, and the step's q, u on demand from the order kernel's X, U snapshot (the ordered
+    launch leaves the snapshot to mpcq_order.hip): every output and the device view's q, u bit-identical to
+    index order (MPCQ_ORDER=0, whose tile launch takes the snapshot itself), q, u within 1e-12 of the
+    oracle's (ModelPredictiveControlAPI.cpp:96-99)."""
+    import torch
+    N, B = 20, 10001
+    ops, X, U, q, u = _problem(plant, N, B, seed=5)
+    l = np.full(2 * N, LMIN)
+
+    def run(order):
+        if order:
+            monkeypatch.delenv("MPCQ_ORDER", raising=False)
+        else:
+            monkeypatch.setenv("MPCQ_ORDER", "0")
+        s = sm.BatchSolver(N, 2 * N, B, dtype=dtype)
+        s.setup(ops["P"], np.zeros(N), ops["A"], l, oracle.upper_bound(ops, np.zeros(4), 0.0))
+        s.mpc_set_operators(ops["Fx"], ops["Fu"], ops["Fr"], ops["Sbar"], ops["Ku"], ops["W0"])
+        Xd, Ud = torch.from_numpy(X.copy()).cuda(), torch.from_numpy(U.copy()).cuda()
+        s.mpc_step_device(Xd.data_ptr(), Ud.data_ptr(), 0.0)
+        torch.cuda.synchronize()
+        assert s.path()[0] == "tile"
+        o = s.order()[0]
+        v = s.device_view()
+        torch.cuda.synchronize()
+        qd = torch.as_tensor(_DevArray(v["q"], (B, N)), device="cuda").cpu().numpy()
+        ud = torch.as_tensor(_DevArray(v["u"], (B, 2 * N)), device="cuda").cpu().numpy()
+        out = (Ud.cpu().numpy(), s.solution(), s.dual(), *s.info(), qd, ud)
+        s.close()
+        return o, out
+
+    o1, got = run(True)
+    o0, ref = run(False)
+    assert o1 and not o0
+    for a_, b_ in zip(got, ref):
+        assert np.array_equal(a_, b_, equal_nan=True)
+    qd, ud = got[-2], got[-1]
+    assert np.abs(qd - q).max() <= 1e-12 * max(1.0, np.abs(q).max())
+    assert np.abs(ud - u).max() <= 1e-12 * max(1.0, np.abs(u).max())
+
+
 @pytest.mark.parametrize("dtype", ["f32", "f64", "mixed"])
 def test_hardest_first_order_is_transparent(plant, dtype, monkeypatch):
     """The tile path's hardest-first MPC step (mpcq_order.hip: the batch run in ascending |max_j (A x_u -
