@@ -509,15 +509,21 @@ __global__ __launch_bounds__(kMimoSetupThreads, 8) void mimo_setup_kernel(MimoSe
         out[L.cs] = cst;
         out[L.cs + 1] = 1.0 / cst;
     }
+    // SW: the terms s_k (c1, c2) = sum_r K0(r, c1) K0(r, c2) 2 E(k, r)^2 of every k at once (into the Ruiz
+    // partials' space, dead by now), then one suffix sum over k per (c1, c2), k descending as before
     for (int it = t; it < N * nu * nu; it += T) {
-        const int j = it / (nu * nu), c1 = (it / nu) % nu, c2 = it % nu;
+        const int k = it / (nu * nu), c1 = (it / nu) % nu, c2 = it % nu;
+        double sk = 0.0;
+        for (int r = 0; r < nu; r++) sk += K0[r * nu + c1] * K0[r * nu + c2] * (2.0 * Ev[k * nu + r] * Ev[k * nu + r]);
+        cm[it] = sk;
+    }
+    __syncthreads();
+    for (int it = t; it < nu * nu; it += T) {
         double acc = 0.0;
-        for (int k = N - 1; k >= j; k--) {
-            double s = 0.0;
-            for (int r = 0; r < nu; r++) s += K0[r * nu + c1] * K0[r * nu + c2] * (2.0 * Ev[k * nu + r] * Ev[k * nu + r]);
-            acc += s;
+        for (int k = N - 1; k >= 0; k--) {
+            acc += cm[k * nu * nu + it];
+            out[L.SW + k * nu * nu + it] = acc;
         }
-        out[L.SW + it] = acc;
     }
     MPCQ_SSTAMP(7);
     if (a.stamps && t == 0) a.stamps[(size_t)pl * 16 + 15] = (long long)__builtin_amdgcn_s_memrealtime();
