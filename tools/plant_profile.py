@@ -22,8 +22,9 @@ t = lambda v: torch.as_tensor(np.ascontiguousarray(v, dtype=np.float64), device=
 pl = [t(Ad), t(Bd), t(np.tile(plant["Cd"], (B, 1))), t(np.tile(plant["K"], (B, 1))), t(np.full(B, plant["Q"])),
       t(np.full(B, plant["R"])), t(np.full(B, plant["RD"]))]
 Xd, U0 = t(X), t(U)
-for dtype in ("f32", "f64"):
+for dtype in os.environ.get("DTYPES", "f32,f64").split(","):
     for name, over in (("default", {}), ("max_iter=1", dict(max_iter=1)), ("scaling=0,max_iter=1", dict(scaling=0, max_iter=1)),
+                       ("max_iter=25", dict(max_iter=25)), ("max_iter=24", dict(max_iter=24)),
                        ("no_adapt", dict(adaptive_rho=0))):
         s = sm.BatchSolver(N, 2 * N, B, n_plants=B, dtype=dtype, settings=sm.default_settings(**over))
         Ud = U0.clone()
