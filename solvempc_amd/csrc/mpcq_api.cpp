@@ -55,6 +55,8 @@ constexpr int kMaxPhases = 16;
 //   MPCQ_PLANT_LAYOUT=2         the one-pass per-plant kernel with two plants per wave at N 17 .. 20 (default 3)
 //   MPCQ_ORDER=0                a shared-plant MPC step's tile solve in index order (default: hardest first)
 //   MPCQ_LAZY_XY=0              the tile solve stores x, y at finalize (default: published on demand)
+//   MPCQ_LAZY_INFO=0            an ordered one-launch solve stores status, iter at the QPs' indices
+//                               (default: in list-slot order, permuted on demand)
 // Debug builds (-DMPCQ_DEBUG_HOOKS) add the stamp / profiling dumps (MPCQ_TILE_STAMPS,
 // MPCQ_SETUP_PROF, MPCQ_MIMO_SETUP_STAMPS, MPCQ_MIMO_STAMPS) and MPCQ_DEBUG_SYNC.
 const char *test_hook(const char *name)
@@ -145,7 +147,9 @@ struct mpcq_ctx {
     // violation map of plant 0, the bin counters and lists; ord_ok when the map matches the current setup
     // and operators
     double *d_ordmap = nullptr;
-    int *d_ord = nullptr;  // OrderBins::kBins counters, then kBins lists of `batch` entries
+    // OrderBins::kBins counters, then `batch` keys, the list of `batch` QPs, and `batch` (status, iter) pairs in
+    // list-slot order (AdmmArgs::info_slot)
+    int *d_ord = nullptr;
     bool ord_ok = false;
     bool ord_last = false;  // the last solve ran in that order (mpcq_get_order)
     bool ord_clean = false;  // its bin counters are zero (an ordered phase-0 launch clears them)
@@ -157,6 +161,10 @@ struct mpcq_ctx {
     // from it by materialize_rho before anything reads d_rho (get_info, the device view, verbose) or a
     // reset overwrites d_rhos
     bool rho_lazy = false;
+    // an ordered single-launch solve left status, iter in list-slot order: materialize_info permutes them
+    // into d_status, d_iter before anything reads those (get_info, the device view, verbose, the publish
+    // kernel of materialize_xy)
+    bool info_lazy = false;
     // host copies of plant-0 scaling
     std::vector<double> hD, hE;
     double hc = 1.0;
@@ -164,6 +172,7 @@ struct mpcq_ctx {
 
 static int materialize_xy(mpcq_ctx *c);  // (below: the lazy x, y of a tile solve)
 static int materialize_rho(mpcq_ctx *c);  // (and its rho)
+static int materialize_info(mpcq_ctx *c);  // (and its status, iter)
 
 namespace {
 
@@ -854,6 +863,10 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
         // fp64 state: the finalize stores rho once, as warm state (materialize_rho reports it)
         if (std::is_same<T, double>::value) a.rho_out = nullptr;
     }
+    // ... and one ordered launch its status, iter in list-slot order (materialize_info; test hook
+    // MPCQ_LAZY_INFO=0: at the QPs' indices)
+    const bool lazy_info = lazy_xy && ordered && np == 1 && test_hook("MPCQ_LAZY_INFO")[0] != '0';
+    a.info_slot = lazy_info ? ord_list + B : nullptr;
 
     // debug build: per-wave stage stamps of every phase launch, written to $MPCQ_TILE_STAMPS after the solve
     const char *stp = debug_hook("MPCQ_TILE_STAMPS");
@@ -908,6 +921,7 @@ static int launch_phases(mpcq_ctx *c, mpcq::AdmmArgs<T> &a, hipStream_t s, bool 
     }
     c->xy_lazy = lazy_xy;
     c->rho_lazy = lazy_xy && std::is_same<T, double>::value;
+    c->info_lazy = lazy_info;
     if (stp && *stp) {
         std::vector<long long> h(8 * waves * kMaxPhases);
         if (hipMemcpyAsync(h.data(), c->d_stamps, 8 * h.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -1033,7 +1047,8 @@ static void verbose_solve(mpcq_ctx *c, double seconds)
     const size_t B = c->dims.batch, n = c->dims.n, m = c->dims.m;
     std::vector<int> st(B), it(B);
     std::vector<double> rho(B), x(n), y(m), q(n), u(m), l(m), P(n * n), A(m * n);
-    if (materialize_xy(c) != MPCQ_OK || materialize_rho(c) != MPCQ_OK || hipStreamSynchronize(c->last) != hipSuccess ||
+    if (materialize_xy(c) != MPCQ_OK || materialize_rho(c) != MPCQ_OK || materialize_info(c) != MPCQ_OK ||
+        hipStreamSynchronize(c->last) != hipSuccess ||
         hipMemcpy(st.data(), c->d_status, 4 * B, hipMemcpyDeviceToHost) != hipSuccess ||
         hipMemcpy(it.data(), c->d_iter, 4 * B, hipMemcpyDeviceToHost) != hipSuccess ||
         hipMemcpy(rho.data(), c->d_rho, 8 * B, hipMemcpyDeviceToHost) != hipSuccess ||
@@ -1099,6 +1114,7 @@ static int launch_solve(mpcq_ctx *c, hipStream_t s, bool mpc, const double *X, d
     c->ord_last = false;  // (launch_phases sets it for a hardest-first tile solve)
     c->xy_lazy = false;   // (and this, for a chain that publishes x, y lazily)
     c->rho_lazy = false;  // (the solve below writes d_rho, or leaves it lazy again)
+    c->info_lazy = false;  // (and d_status, d_iter: every solve writes every QP's)
     const int rc = c->dims.dtype == MPCQ_F32 ? launch_typed<float>(c, s, mpc, X, U, xref)
                                              : launch_typed<double>(c, s, mpc, X, U, xref);
     if (rc) return fail(MPCQ_ERR_HIP, std::string("ADMM kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
@@ -1163,6 +1179,7 @@ int mpcq_get_info(mpcq_ctx *c, int *status, int *iter, double *rho)
     if (rc) return rc;
     const size_t B = c->dims.batch;
     if (rho && (rc = materialize_rho(c))) return rc;
+    if ((status || iter) && (rc = materialize_info(c))) return rc;
     if ((rc = d2h(c, status, c->d_status, 4 * B))) return rc;
     if ((rc = d2h(c, iter, c->d_iter, 4 * B))) return rc;
     return d2h(c, rho, c->d_rho, 8 * B);
@@ -1214,7 +1231,7 @@ int mpcq_device_view_get(mpcq_ctx *c, mpcq_device_view *v)
 {
     if (!c || !v) return fail(MPCQ_ERR_ARG, "null argument");
     int rc = materialize_qu(c);  // (enqueued on the context's last stream)
-    if (rc || (rc = materialize_xy(c)) || (rc = materialize_rho(c))) return rc;
+    if (rc || (rc = materialize_xy(c)) || (rc = materialize_rho(c)) || (rc = materialize_info(c))) return rc;
     v->q = c->d_q;
     v->u = c->d_u;
     v->l = c->d_l;
@@ -1263,7 +1280,8 @@ static int materialize_xy(mpcq_ctx *c)
 {
     if (!c->xy_lazy) return MPCQ_OK;
     c->xy_lazy = false;
-    int rc;
+    int rc = materialize_info(c);  // (the publish kernel reads each QP's status)
+    if (rc) return rc;
     if (c->dims.dtype == MPCQ_F32) {
         auto a = make_args<float>(c);
         a.img = (const float *)c->d_img;
@@ -1282,6 +1300,18 @@ static int materialize_rho(mpcq_ctx *c)
     if (!c->rho_lazy) return MPCQ_OK;
     c->rho_lazy = false;
     HIPCHK(hipMemcpyAsync(c->d_rho, c->d_rhos, 8 * (size_t)c->dims.batch, hipMemcpyDeviceToDevice, c->last));
+    return MPCQ_OK;
+}
+
+// d_status, d_iter of the last ordered single-launch solve from its list-slot pairs, once.
+static int materialize_info(mpcq_ctx *c)
+{
+    if (!c->info_lazy) return MPCQ_OK;
+    c->info_lazy = false;
+    const int B = c->dims.batch;
+    const int *list = c->d_ord + mpcq::OrderBins::kBins + B;
+    if (mpcq_internal_order_info(B, list, list + B, c->d_status, c->d_iter, c->last) != 0)
+        return fail(MPCQ_ERR_HIP, "status publish kernel failed");
     return MPCQ_OK;
 }
 
@@ -1361,7 +1391,7 @@ static int build_order_map(mpcq_ctx *c)
         for (int k = 0; k < KS; k++)
             if (!std::isfinite(row[k])) return MPCQ_OK;
     }
-    const size_t ord_ints = (size_t)mpcq::OrderBins::kBins + 2 * (size_t)c->dims.batch;  // counters, keys, list
+    const size_t ord_ints = (size_t)mpcq::OrderBins::kBins + 4 * (size_t)c->dims.batch;  // counters, keys, list, info
     if (!c->d_ordmap && hipMalloc((void **)&c->d_ordmap, 8 * (size_t)mpcq::OrderBins::kMaxRows * KS) != hipSuccess)
         return fail(MPCQ_ERR_HIP, "hipMalloc failed (order map)");
     if (!c->d_ord) {
@@ -1471,6 +1501,7 @@ static int launch_stream(mpcq_ctx *c, hipStream_t s, double *X, double *U, doubl
 {
     c->xy_lazy = false;  // (the stream writes every QP's x, y at its last step)
     c->rho_lazy = false;  // (and rho)
+    c->info_lazy = false;  // (and status, iter)
     auto a = make_args<T>(c);
     a.mpc = 1; a.mpc_u = 1; a.nx = c->nx; a.X = X; a.U = U; a.xref = xref;
     a.Fx = c->d_Fx; a.Fu = c->d_Fu; a.Fr = c->d_Fr; a.Sbar = c->d_Sbar; a.Ku = c->d_Ku; a.W0 = c->d_W0;
@@ -1495,6 +1526,7 @@ static int launch_tile_stream(mpcq_ctx *c, hipStream_t s, double *X, double *U, 
 {
     c->xy_lazy = false;  // (the stream writes every QP's x, y at its last step)
     c->rho_lazy = false;  // (and rho)
+    c->info_lazy = false;  // (and status, iter)
     const mpcq_settings &st = c->set;
     const int ct = st.check_termination;
     auto a = make_args<T>(c);

@@ -239,6 +239,11 @@ struct AdmmArgs {
     // (T) eps_abs, eps_rel, eps_prim_inf, eps_dual_inf times T(10), formed on the host in T: the tile
     // kernel's approximate check_termination (OSQP auxil.c, the 10x tolerances after max_iter)
     T eps10[4];
+    // a hardest-first solve in one launch: the finalize stores (status, iter) of list slot i at
+    // info_slot[2 i], [2 i + 1], one 8-B store per QP into the wave's own 128-B line, instead of two
+    // scattered 4-B stores at the QP's index (mpcq_api.cpp materialize_info permutes them when read); null:
+    // at the QP's index in status, iter
+    int *info_slot;
 };
 
 // MFMA operand images of one shared plant for the tile kernel (mpcq_tile.h).  A vector of length
@@ -439,6 +444,8 @@ int mpcq_internal_set_step(long long *step, long long v, hipStream_t s);
 // (or null): copies of X, U for the step's q, u on demand.
 int mpcq_internal_order(int batch, int nx, int m, const double *X, const double *U, const double *kmap, double xref,
                         int *cnt, int *key, int *list, double *Xs, double *Us, hipStream_t s);
+// status[list[i]], iter[list[i]] = slot[2 i], slot[2 i + 1] (an ordered launch's AdmmArgs::info_slot)
+int mpcq_internal_order_info(int batch, const int *list, const int *slot, int *status, int *iter, hipStream_t s);
 // MIMO condensed MPC (mpcq_mimo.hip): per-plant condensing + Ruiz + P^, then the per-QP solve
 // (one 512-thread workgroup per QP: KKT inverse by Gauss-Jordan in VGPRs, structured A).
 int mpcq_internal_mimo_setup_launch(const mpcq::MimoSetupArgs *a, hipStream_t s);

@@ -126,7 +126,31 @@ __global__ __launch_bounds__(256) void order_scatter_kernel(int batch, const int
     }
 }
 
+// (status, iter) of an ordered single-launch solve from list-slot order to the QPs' indices
+// (AdmmArgs::info_slot): status[list[i]], iter[list[i]] = slot i's pair
+__global__ __launch_bounds__(256) void order_info_kernel(int batch, const int *__restrict__ list,
+                                                         const int2 *__restrict__ slot, int *__restrict__ status,
+                                                         int *__restrict__ iter)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= batch) return;
+    const int b = list[i];
+    if (b < 0 || b >= batch) return;  // (never: the list is a permutation of the batch)
+    const int2 v = slot[i];
+    status[b] = v.x;
+    iter[b] = v.y;
+}
+
 }  // namespace mpcq
+
+extern "C" int mpcq_internal_order_info(int batch, const int *list, const int *slot, int *status, int *iter,
+                                        hipStream_t s)
+{
+    if (batch <= 0) return 0;
+    hipLaunchKernelGGL(mpcq::order_info_kernel, dim3((batch + 255) / 256), dim3(256), 0, s, batch, list,
+                       (const int2 *)slot, status, iter);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
 
 // cnt: OrderBins::kBins counters, zero on entry (cleared by the previous ordered tile launch, or by the
 // caller); key: batch ints of scratch; list: batch ints, the QPs hardest first; Xs, Us (or null): copies of

@@ -845,8 +845,14 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 }
             if (g == 0) {
                 o_rhos[b] = rho[gi];
-                o_status[b] = sta;
-                o_iter[b] = it - cst[gi];
+                if (!STREAM && a.info_slot) {  // (ordered single launch: slot = the list entry this column runs)
+                    const int col = opaque((int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u))) & 15;
+                    const int slot = (blk * WPB + ((int)threadIdx.x >> 6)) * 16 * G + 16 * gi + col;
+                    *(int2 *)(fresh_ptr(a.info_slot) + 2 * (size_t)slot) = make_int2(sta, it - cst[gi]);
+                } else {
+                    o_status[b] = sta;
+                    o_iter[b] = it - cst[gi];
+                }
                 if (a.rho_out) o_rho[b] = (double)rho[gi];  // (null: the fp64 rhos above is reported, mpcq_api.cpp
                                                             // materialize_rho)
                 if (a.it_acc) {

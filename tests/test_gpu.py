@@ -996,8 +996,8 @@ def test_paired_tile_path_selected(plant):
 class _DevArray:
     """A device buffer of the C ABI's device view, wrapped for torch (__cuda_array_interface__)."""
 
-    def __init__(self, ptr, shape):
-        self.__cuda_array_interface__ = {"shape": shape, "typestr": "<f8", "data": (ptr, False), "version": 3}
+    def __init__(self, ptr, shape, typestr="<f8"):
+        self.__cuda_array_interface__ = {"shape": shape, "typestr": typestr, "data": (ptr, False), "version": 3}
 
 
 @pytest.mark.parametrize("dtype", ["f32", "f64"])
@@ -1237,6 +1237,54 @@ def test_ordered_step_ragged_batch_and_snapshot(plant, dtype, monkeypatch):
     qd, ud = got[-2], got[-1]
     assert np.abs(qd - q).max() <= 1e-12 * max(1.0, np.abs(q).max())
     assert np.abs(ud - u).max() <= 1e-12 * max(1.0, np.abs(u).max())
+
+
+@pytest.mark.parametrize("dtype", ["f64", "mixed"])
+def test_ordered_step_lazy_info(plant, dtype, monkeypatch):
+    """A hardest-first step in one launch stores (status, iter) in list-slot order, one 8-B store per QP
+    into its wave's line (AdmmArgs::info_slot), and mpcq_api.cpp materialize_info permutes them when read:
+    bit-identical to the stores at the QPs' indices (MPCQ_LAZY_INFO=0) whichever reader comes first
+    (get_info; get_solution, whose publish kernel reads the status; the device view), and a step that
+    nobody read is superseded by the next one (10,001 QPs: a ragged last wave)."""
+    import torch
+    N, B = 20, 10001
+    ops, X, U, q, u = _problem(plant, N, B, seed=7)
+    X2 = workload.mpc_states(8, 0, B, 1.0)[0]
+    l = np.full(2 * N, LMIN)
+
+    def run(lazy):
+        if lazy:
+            monkeypatch.delenv("MPCQ_LAZY_INFO", raising=False)
+        else:
+            monkeypatch.setenv("MPCQ_LAZY_INFO", "0")
+        s = sm.BatchSolver(N, 2 * N, B, dtype=dtype)
+        s.setup(ops["P"], np.zeros(N), ops["A"], l, oracle.upper_bound(ops, np.zeros(4), 0.0))
+        s.mpc_set_operators(ops["Fx"], ops["Fu"], ops["Fr"], ops["Sbar"], ops["Ku"], ops["W0"])
+        Xd, Ud = torch.from_numpy(X.copy()).cuda(), torch.from_numpy(U.copy()).cuda()
+        out = []
+        s.mpc_step_device(Xd.data_ptr(), Ud.data_ptr(), 0.0)  # step 1: info read first
+        out += [*s.info(), s.solution()]
+        s.mpc_step_device(Xd.data_ptr(), Ud.data_ptr(), 0.0)  # step 2: the solution read first
+        out += [s.solution(), *s.info()]
+        s.mpc_step_device(Xd.data_ptr(), Ud.data_ptr(), 0.0)  # step 3: nobody reads it
+        Xd.copy_(torch.from_numpy(X2))
+        s.mpc_step_device(Xd.data_ptr(), Ud.data_ptr(), 0.0)  # step 4: through the device view
+        o = s.order()[0]
+        v = s.device_view()
+        torch.cuda.synchronize()
+        out += [torch.as_tensor(_DevArray(v[k], (B,), "<i4"), device="cuda").cpu().numpy().copy()
+                for k in ("status", "iter")]
+        out += [Ud.cpu().numpy(), s.dual()]
+        s.close()
+        return o, out
+
+    o1, got = run(True)
+    o0, ref = run(False)
+    assert o1 and o0  # both ran hardest-first; only the info stores differ
+    for a_, b_ in zip(got, ref):
+        assert np.array_equal(a_, b_, equal_nan=True)
+    st4, it4 = got[-4], got[-3]
+    assert (st4 == sm.SOLVED).mean() > 0.99 and it4.max() <= 4000
 
 
 @pytest.mark.parametrize("dtype", ["f32", "f64", "mixed"])
