@@ -135,6 +135,9 @@ struct mpcq_ctx {
     unsigned long long gen = 1;
     struct { double *X, *U; double xref, noise; unsigned long long seed; long long first_qp; hipStream_t s;
              unsigned long long gen; } gkey{};
+    // what the captured step leaves lazy (x, y; rho; status, iter; q, u) and its order flag: every replay
+    // leaves the same, whatever a reader materialised in between
+    struct { bool xy, rho, info, qu, ord; double xref; } glazy{};
     // MIMO condensed MPC (mpcq_mimo.hip): per-plant operator block, dims
     double *d_mimo = nullptr;
     int mimo_N = 0, mimo_nx = 0, mimo_nu = 0, mimo_ny = 0, mimo_srows = 0, mimo_diag_k0 = 0;
@@ -1658,10 +1661,17 @@ int mpcq_mpc_run_device(mpcq_ctx *c, double *X, double *U, double xref, int step
             return fail(MPCQ_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
         }
         c->gkey = {X, U, xref, noise_std, seed, first_qp, s, c->gen};
+        c->glazy = {c->xy_lazy, c->rho_lazy, c->info_lazy, c->qu_lazy, c->ord_last, c->lazy_xref};
     }
     for (int k = done; k < steps; k++) {
         const auto t0 = std::chrono::steady_clock::now();
         HIPCHK(hipGraphLaunch(c->gexec, s));
+        c->xy_lazy = c->glazy.xy;
+        c->rho_lazy = c->glazy.rho;
+        c->info_lazy = c->glazy.info;
+        c->qu_lazy = c->glazy.qu;
+        c->ord_last = c->glazy.ord;
+        c->lazy_xref = c->glazy.xref;
         if (sync_each && (rc = stage(("graph replay " + std::to_string(k)).c_str()))) return rc;
         if (c->set.verbose) {  // (the captured solve printed nothing: launch_solve)
             HIPCHK(hipStreamSynchronize(s));

@@ -604,8 +604,9 @@ def test_stream_one_launch_matches_graph(plant, dtype, family, monkeypatch):
     the same kernel family, from the same cold state: the tile kernel's stream mode (every MFMA column
     one plant running its own control steps, a few plants per wave) against per-step tile solves, and
     stream_wave_kernel (one QP per wave) against per-step wave solves.  Bit-identical X, U, statuses,
-    iterations, rho and stream counters after 30 steps in one call, then 7 more steps in a second call
-    (warm state carried across calls), on a ragged batch."""
+    iterations, rho, stream counters and the last step's x, y after 30 steps in one call, then 7 more steps
+    in a second call (warm state carried across calls; the graph's replays leave the captured step's lazy
+    publication pending again after the first call's reads), on a ragged batch."""
     import torch
     monkeypatch.setenv("MPCQ_KERNEL", family)
     N, B = 20, 333
@@ -631,7 +632,8 @@ def test_stream_one_launch_matches_graph(plant, dtype, family, monkeypatch):
                 s.mpc_run_device(Xd.data_ptr(), Ud.data_ptr(), 0.0, steps, 4, 0, first, 1e-2, st.cuda_stream)
             st.synchronize()
             it_acc, uns = s.stream_counters()
-            out.append((Xd.cpu().numpy().copy(), Ud.cpu().numpy().copy(), *s.info(), it_acc, uns))
+            out.append((Xd.cpu().numpy().copy(), Ud.cpu().numpy().copy(), *s.info(), it_acc, uns, s.solution(),
+                        s.dual()))
             assert s.stream_path() == (mode or family)
         return out
 
