@@ -295,7 +295,7 @@ template <int NC> struct PlantLds {
     static_assert(NP % 2 == 0, "16-B aligned vectors");
     double u[NU];
     double CS[NC], tmp[NC];
-    double sh[4];  // cost, 1 / cost, U, K0
+    double sh[6];  // cost, 1 / cost, U, K0, max |q^|, max |D^-1 q^| (the checks' constant norms)
     __device__ double *V() { return u; }
     __device__ double *Cr() { return u + (NC + 1) * 8; }
     __device__ double *G() { return u; }
@@ -556,11 +556,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         S.Ut()[r] = up_t;
         S.Ub()[r] = up_b;
     }
-    if (r == 0) {
-        S.sh[0] = cost;
-        S.sh[1] = cinv;
-        S.sh[2] = Uv;
-        S.sh[3] = K0;
+    {
+        // |q^| in both scalings: q does not change during the solve, so every check reads these (the check's
+        // own arithmetic: DiD = 1 / D_r, the max over the plant's steps)
+        const double qd = (double)qh, DiD = 1.0 / (lr ? Dr : 1.0);
+        const double qn_r = l_max<LAY>(lr ? fabs(qd) : 0.0, lane), qn_s = l_max<LAY>(lr ? fabs(DiD * qd) : 0.0, lane);
+        if (r == 0) {
+            S.sh[0] = cost;
+            S.sh[1] = cinv;
+            S.sh[2] = Uv;
+            S.sh[3] = K0;
+            S.sh[4] = qn_r;
+            S.sh[5] = qn_s;
+        }
     }
     // the update's checks (l^ = -DBL_MAX E stays free of -OSQP_INFTY MIN_SCALING): u < l cannot occur;
     // a row whose u^ reaches OSQP_INFTY MIN_SCALING would change type (TYPE_CHANGED)
@@ -759,7 +767,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         const TD aty = DKd * l_ssum<LAY>(Ed * (ytd - ybd), lane);
         const TD px = p_times(xs);
         TD ax_z = 0, ax_zs = 0, zn_s = 0, zn_r = 0, axn_s = 0, axn_r = 0;
-        TD dr_r = 0, dr_s = 0, qn_r = 0, qn_s = 0, atyn_r = 0, atyn_s = 0, pxn_r = 0, pxn_s = 0;
+        TD dr_r = 0, dr_s = 0, atyn_r = 0, atyn_s = 0, pxn_r = 0, pxn_s = 0;
+        const TD qn_r = C.sh[4], qn_s = C.sh[5];
         if (lr) {
             const TD r1 = ax - ztd, r2 = -ax - zbd;
             ax_z = hwmax_abs2(r1, r2);
@@ -771,18 +780,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
             const TD rd = (qsl + px) + aty;
             dr_r = fabs(rd);
             dr_s = fabs(DiD * rd);
-            qn_r = fabs(qsl);
-            qn_s = fabs(DiD * qsl);
             atyn_r = fabs(aty);
             atyn_s = fabs(DiD * aty);
             pxn_r = fabs(px);
             pxn_s = fabs(DiD * px);
         }
         auto pmax = [&](TD v) { return l_max<LAY>(v, lane); };
-        ax_z = pmax(ax_z); ax_zs = pmax(ax_zs); zn_s = pmax(zn_s); zn_r = pmax(zn_r);
-        axn_s = pmax(axn_s); axn_r = pmax(axn_r);
-        dr_r = pmax(dr_r); dr_s = pmax(dr_s); qn_r = pmax(qn_r); qn_s = pmax(qn_s);
-        atyn_r = pmax(atyn_r); atyn_s = pmax(atyn_s); pxn_r = pmax(pxn_r); pxn_s = pmax(pxn_s);
+        // the norms in the scaling the termination test reads (scaled_termination: OSQP's scaled residuals,
+        // else the unscaled ones), and the scaled ones adapt_rho reads: only the sets this iteration uses
+        // (wave-uniform; with the default intervals three checks in four test termination only)
+        if (scaled_term || at_adapt) {
+            ax_z = pmax(ax_z); zn_r = pmax(zn_r); axn_r = pmax(axn_r);
+            dr_r = pmax(dr_r); atyn_r = pmax(atyn_r); pxn_r = pmax(pxn_r);
+        }
+        if (!scaled_term && (at_check || last)) {
+            ax_zs = pmax(ax_zs); zn_s = pmax(zn_s); axn_s = pmax(axn_s);
+            dr_s = pmax(dr_s); atyn_s = pmax(atyn_s); pxn_s = pmax(pxn_s);
+        }
         const TD pri_res = scaled_term ? ax_z : ax_zs;
         const TD dua_res = scaled_term ? dr_r : cinvl * dr_s;
 
