@@ -154,6 +154,10 @@ struct mpcq_ctx {
     // list-slot order (AdmmArgs::info_slot)
     int *d_ord = nullptr;
     bool ord_ok = false;
+    // the same order for a batch of distinct plants (mpcq_mpc_plants_step_device): the map of the batch's first
+    // plant, kept while the plant arrays are the same (pord_key); pord_ok when d_ordmap holds it
+    bool pord_ok = false;
+    struct { const double *Ad, *Bd, *Cd, *K, *Q, *R, *RD; int nx, s_rows; } pord_key{};
     bool ord_last = false;  // the last solve ran in that order (mpcq_get_order)
     bool ord_clean = false;  // its bin counters are zero (an ordered phase-0 launch clears them)
     // a tile solve whose finalize stored only the warm state (x', z, y) and U: d_x, d_y are formed from it by
@@ -1325,25 +1329,13 @@ static int materialize_info(mpcq_ctx *c)
 // Host fp64 (Cholesky of plant 0's P, upper triangle as OSQP reads it), once per setup / operator set;
 // the map only orders the batch (no result depends on it), so a P that is not positive definite or a
 // shape the kernel does not take just leaves the order off.
-static int build_order_map(mpcq_ctx *c)
+// The order map's rows from one plant's condensed operators (host fp64): false when P is not positive
+// definite or a row is not finite (no order then).
+static bool order_map_rows(int n, int m, int nx, const std::vector<double> &P, const std::vector<double> &A,
+                           const std::vector<double> &Fx, const std::vector<double> &Fu, const std::vector<double> &Fr,
+                           const std::vector<double> &Sb, const std::vector<double> &Ku, const std::vector<double> &W0,
+                           std::vector<double> &map)
 {
-    c->ord_ok = false;
-    const int n = c->dims.n, m = c->dims.m, nx = c->nx;
-    if (!c->tile || !c->mpc_ready || c->dims.n_plants != 1 || c->mode != mpcq_ctx::Mode::Generic || nx <= 0 ||
-        nx > 8 || m > mpcq::OrderBins::kMaxRows)
-        return MPCQ_OK;
-    std::vector<double> P((size_t)n * n), A((size_t)m * n), Fx((size_t)n * nx), Fu(n), Fr((size_t)n * n),
-        Sb((size_t)m * nx), Ku(m), W0(m);
-    hipStream_t s = c->last;
-    HIPCHK(hipMemcpyAsync(P.data(), c->d_P, 8 * P.size(), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(A.data(), c->d_A, 8 * A.size(), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(Fx.data(), c->d_Fx, 8 * Fx.size(), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(Fu.data(), c->d_Fu, 8 * Fu.size(), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(Fr.data(), c->d_Fr, 8 * Fr.size(), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(Sb.data(), c->d_Sbar, 8 * Sb.size(), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(Ku.data(), c->d_Ku, 8 * Ku.size(), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(W0.data(), c->d_W0, 8 * W0.size(), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
     // Cholesky P = L L' (lower L in place, from P's upper triangle)
     std::vector<double> L((size_t)n * n, 0.0);
     for (int j = 0; j < n; j++) {
@@ -1351,7 +1343,7 @@ static int build_order_map(mpcq_ctx *c)
             double v = P[(size_t)j * n + i];  // P(j, i), j <= i: upper triangle
             for (int k = 0; k < j; k++) v -= L[(size_t)i * n + k] * L[(size_t)j * n + k];
             if (i == j) {
-                if (!(v > 0.0)) return MPCQ_OK;  // not positive definite: no order
+                if (!(v > 0.0)) return false;  // not positive definite: no order
                 L[(size_t)j * n + j] = std::sqrt(v);
             } else {
                 L[(size_t)i * n + j] = v / L[(size_t)j * n + j];
@@ -1381,7 +1373,7 @@ static int build_order_map(mpcq_ctx *c)
         }
     }
     constexpr int KS = mpcq::OrderBins::kStride;
-    std::vector<double> map((size_t)m * KS, 0.0);
+    map.assign((size_t)m * KS, 0.0);
     for (int j = 0; j < m; j++) {
         double az[10] = {0};
         for (int r = 0; r < nr; r++)
@@ -1392,8 +1384,15 @@ static int build_order_map(mpcq_ctx *c)
         row[9] = -W0[j];
         row[10] = -az[nx + 1];
         for (int k = 0; k < KS; k++)
-            if (!std::isfinite(row[k])) return MPCQ_OK;
+            if (!std::isfinite(row[k])) return false;
     }
+    return true;
+}
+
+// The map to the device, with the order's counters and lists (allocated once per context).
+static int upload_order_map(mpcq_ctx *c, const std::vector<double> &map, hipStream_t s)
+{
+    constexpr int KS = mpcq::OrderBins::kStride;
     const size_t ord_ints = (size_t)mpcq::OrderBins::kBins + 4 * (size_t)c->dims.batch;  // counters, keys, list, info
     if (!c->d_ordmap && hipMalloc((void **)&c->d_ordmap, 8 * (size_t)mpcq::OrderBins::kMaxRows * KS) != hipSuccess)
         return fail(MPCQ_ERR_HIP, "hipMalloc failed (order map)");
@@ -1404,7 +1403,33 @@ static int build_order_map(mpcq_ctx *c)
         c->gen++;
     }
     if (int rc2 = h2d(c->d_ordmap, map.data(), 8 * map.size(), s)) return rc2;
+    return MPCQ_OK;
+}
+
+static int build_order_map(mpcq_ctx *c)
+{
+    c->ord_ok = false;
+    const int n = c->dims.n, m = c->dims.m, nx = c->nx;
+    if (!c->tile || !c->mpc_ready || c->dims.n_plants != 1 || c->mode != mpcq_ctx::Mode::Generic || nx <= 0 ||
+        nx > 8 || m > mpcq::OrderBins::kMaxRows)
+        return MPCQ_OK;
+    std::vector<double> P((size_t)n * n), A((size_t)m * n), Fx((size_t)n * nx), Fu(n), Fr((size_t)n * n),
+        Sb((size_t)m * nx), Ku(m), W0(m);
+    hipStream_t s = c->last;
+    HIPCHK(hipMemcpyAsync(P.data(), c->d_P, 8 * P.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(A.data(), c->d_A, 8 * A.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(Fx.data(), c->d_Fx, 8 * Fx.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(Fu.data(), c->d_Fu, 8 * Fu.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(Fr.data(), c->d_Fr, 8 * Fr.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(Sb.data(), c->d_Sbar, 8 * Sb.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(Ku.data(), c->d_Ku, 8 * Ku.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(W0.data(), c->d_W0, 8 * W0.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<double> map;
+    if (!order_map_rows(n, m, nx, P, A, Fx, Fu, Fr, Sb, Ku, W0, map)) return MPCQ_OK;
+    if (int rc = upload_order_map(c, map, s)) return rc;
     c->ord_ok = true;
+    c->pord_ok = false;  // (the map is now this plant's)
     return MPCQ_OK;
 }
 
@@ -1784,6 +1809,48 @@ int mpcq_mpc_setup_plants_device(mpcq_ctx *c, int nx, int s_rows, const double *
 }
 
 
+// The hardest-first map of a batch of distinct plants: the first plant's condensed operators (mpcq_condense,
+// synchronous: once per set of plant arrays), folded as build_order_map folds a shared plant's.  The plants of
+// config 3 are perturbations of one nominal plant (Ad, Bd +-2 %), so one plant's map ranks every QP's
+// unconstrained-optimum violation closely enough to group QPs of like iteration counts in a wave and to run
+// the slow ones first; the map only orders the batch, no result depends on it (a stale map, after the
+// arrays' contents change under the same pointers, costs time only).
+static int plants_order_map(mpcq_ctx *c, int nx, int s_rows, const double *Ad, const double *Bd, const double *Cd,
+                            const double *K, const double *Q, const double *R, const double *RD, hipStream_t s)
+{
+    const int n = c->dims.n, m = c->dims.m;
+    if (c->pord_ok && c->pord_key.Ad == Ad && c->pord_key.Bd == Bd && c->pord_key.Cd == Cd && c->pord_key.K == K &&
+        c->pord_key.Q == Q && c->pord_key.R == R && c->pord_key.RD == RD && c->pord_key.nx == nx &&
+        c->pord_key.s_rows == s_rows)
+        return MPCQ_OK;
+    c->pord_ok = false;
+    c->ord_ok = false;  // (d_ordmap is about to hold the plants' map)
+    if (m > mpcq::OrderBins::kMaxRows || nx > 8) return MPCQ_OK;
+    std::vector<double> in((size_t)nx * nx + 3 * nx + 3);
+    double *hAd = in.data(), *hBd = hAd + nx * nx, *hCd = hBd + nx, *hK = hCd + nx, *hQ = hK + nx;
+    HIPCHK(hipMemcpyAsync(hAd, Ad, 8 * (size_t)nx * nx, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hBd, Bd, 8 * (size_t)nx, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hCd, Cd, 8 * (size_t)nx, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hK, K, 8 * (size_t)nx, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hQ, Q, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hQ + 1, R, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hQ + 2, RD, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<double> P((size_t)n * n), A((size_t)m * n), Fx((size_t)n * nx), Fu(n), Fr((size_t)n * n),
+        Sb((size_t)m * nx), Ku(m), W0(m);
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    if (mpcq_condense(dev, 1, nx, n, s_rows, hAd, hBd, hCd, hK, hQ, hQ + 1, hQ + 2, P.data(), A.data(), Fx.data(),
+                      Fu.data(), Fr.data(), Sb.data(), Ku.data(), W0.data()) != MPCQ_OK)
+        return MPCQ_OK;  // (no order: the step itself reports any error with these arrays)
+    std::vector<double> map;
+    if (!order_map_rows(n, m, nx, P, A, Fx, Fu, Fr, Sb, Ku, W0, map)) return MPCQ_OK;
+    if (int rc = upload_order_map(c, map, s)) return rc;
+    c->pord_ok = true;
+    c->pord_key = {Ad, Bd, Cd, K, Q, R, RD, nx, s_rows};
+    return MPCQ_OK;
+}
+
 int mpcq_mpc_plants_step_device(mpcq_ctx *c, int nx, int s_rows, const double *Ad, const double *Bd,
                                 const double *Cd, const double *K, const double *Q, const double *R,
                                 const double *RD, const double *X, double *U, double xref, void *stream)
@@ -1817,8 +1884,27 @@ int mpcq_mpc_plants_step_device(mpcq_ctx *c, int nx, int s_rows, const double *A
         const char *l = test_hook("MPCQ_PLANT_LAYOUT");  // 2: two plants per wave at N 17 .. 20 (A/B, parity)
         a.layout = *l ? std::atoi(l) : 0;
     }
+    // hardest-first (the first plant's map, mpcq_order.hip; test hook MPCQ_PLANT_ORDER=0: index order): slot i
+    // of the grid runs plant list[i], and the kernel's workgroup 0 clears the bin counters for the next sort
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    const bool want = test_hook("MPCQ_PLANT_ORDER")[0] != '0' && c->dims.batch < (1 << mpcq::OrderBins::kRankBits) &&
+                      hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone;
+    if (want && (rc = plants_order_map(c, nx, s_rows, Ad, Bd, Cd, K, Q, R, RD, s))) return rc;
+    const bool ordered = want && c->pord_ok;
+    if (ordered) {
+        const int B = c->dims.batch;
+        int *const cnt = c->d_ord, *const key = cnt + mpcq::OrderBins::kBins, *const list = key + B;
+        if (!c->ord_clean) HIPCHK(hipMemsetAsync(cnt, 0, 4 * (size_t)mpcq::OrderBins::kBins, s));
+        c->ord_clean = false;
+        if (mpcq_internal_order(B, nx, m, X, U, c->d_ordmap, xref, cnt, key, list, nullptr, nullptr, s) != 0)
+            return fail(MPCQ_ERR_HIP, "plants_step order launch failed");
+        a.order = list;
+        a.ord_zero = cnt;
+    }
     const int lr = mpcq_internal_plant_step_launch(&a, c->dims.dtype == MPCQ_F32, s);
     if (lr) return fail(lr == -1 ? MPCQ_ERR_ARG : MPCQ_ERR_HIP, "plants_step kernel launch failed");
+    if (ordered) c->ord_clean = true;
+    c->ord_last = ordered;
     c->mode = mpcq_ctx::Mode::OneShot;  // results only: no operator blocks were written
     c->mpc_ready = false;
     c->last = s;

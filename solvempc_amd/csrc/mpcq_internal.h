@@ -387,6 +387,10 @@ struct PlantStepArgs {
     int wpe;                                       // waves per SIMD of the kernel variant (2; 3: A/B hook)
     int layout;                                    // plants per wave (0: the default, 3 for 17 <= N <= 20;
                                                    // 2: one per 32-lane half, test hook MPCQ_PLANT_LAYOUT)
+    // hardest-first (mpcq_order.hip): slot i of the grid runs plant order[i] (null: plant i); workgroup 0
+    // zeroes the OrderBins::kBins counters ord_zero for the next sort
+    const int *order;
+    int *ord_zero;
 };
 }  // namespace mpcq
 

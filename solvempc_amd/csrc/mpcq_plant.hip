@@ -372,9 +372,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     __shared__ PL lds[LAY];
     __shared__ __attribute__((aligned(16))) T bx[LAY][NC], bw[LAY][NC];  // per-plant broadcasts
     const int lane = threadIdx.x, h = lay_plant<LAY>(lane), r = lay_row<LAY>(lane);
-    const int plant = blockIdx.x * LAY + h;
-    const bool live = plant < a.n_plants;
-    const int p = live ? plant : 0;  // a dead half runs plant 0's data and publishes nothing
+    const int slot = blockIdx.x * LAY + h;
+    const bool live = slot < a.n_plants;
+    // (hardest-first: the slot's plant from the order list, clamped to the batch like the tile kernel's)
+    const int plant = !live ? 0 : (a.order ? min(max(a.order[slot], 0), a.n_plants - 1) : slot);
+    const int p = plant;  // a dead half runs plant 0's data and publishes nothing
+    if (blockIdx.x == 0 && a.ord_zero)  // the order's bin counters, read by its finished sort: the next sort's
+        for (int i = threadIdx.x; i < OrderBins::kBins; i += 64) a.ord_zero[i] = 0;
     const int N = a.N, n = N, nx = a.nx;
     const bool lr = r < N;
     PL &S = lds[h];
@@ -650,7 +654,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     auto finalize = [&]() {
         const int cl = cold_lane(), r = lay_row<LAY>(cl);
         const PL &S = lds[lay_plant<LAY>(cl)];
-        const int plant = blockIdx.x * LAY + lay_plant<LAY>(cl);
+        const int sl = blockIdx.x * LAY + lay_plant<LAY>(cl);
+        const int plant = a.order ? min(max(a.order[sl], 0), a.n_plants - 1) : sl;  // (live: sl < n_plants)
         const bool has_sol = status == kSolved || status == kSolvedInaccurate || status == kMaxIterReached;
         if (!live) return;
         if (lr) {

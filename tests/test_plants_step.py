@@ -181,3 +181,44 @@ def test_full_config3_batch_every_plant(plant, dtype):
     # of its own, within the eps-level gap of the oracle's (up to ~2e-2)
     assert (np.abs(x - x_ref).max(axis=1)[off] / scale[off]).max(initial=0.0) < 5e-2
     print(f"fp32 config 3: {int(off.sum())} of {B} plants took a tie's other branch")
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_hardest_first_plants_are_transparent(plant, dtype, monkeypatch):
+    """The one-pass step runs its batch hardest-first (the first plant's order map, mpcq_api.cpp
+    plants_order_map, and mpcq_order.hip's counting sort; slot i of the grid runs plant list[i]): every
+    output bit-identical to index order (MPCQ_PLANT_ORDER=0) on a ragged batch, the list a permutation of
+    it, and the plants that need the most iterations in its first part.  A second step with the same plant
+    arrays reuses the map (and the bin counters the first step's kernel cleared)."""
+    N, B = 20, 3001
+    Ad, Bd, X, U = _plants(plant, B, 4)
+
+    def run(order):
+        if order:
+            monkeypatch.delenv("MPCQ_PLANT_ORDER", raising=False)
+        else:
+            monkeypatch.setenv("MPCQ_PLANT_ORDER", "0")
+        import torch
+
+        keep = _plant_arrays(plant, Ad, Bd)
+        Xd, Ud = _dev(X), _dev(U)
+        s = sm.BatchSolver(N, 2 * N, B, n_plants=B, dtype=dtype)
+        out = []
+        for _ in range(2):
+            s.mpc_plants_step_device(4, 10, *[k.data_ptr() for k in keep], Xd.data_ptr(), Ud.data_ptr())
+            torch.cuda.synchronize()
+            out += [Ud.cpu().numpy().copy(), s.solution(), s.dual(), *s.info()]
+        o, lst = s.order()
+        s.close()
+        return o, lst, out
+
+    o1, lst, got = run(True)
+    o0, _, ref = run(False)
+    assert o1 and not o0
+    for a_, b_ in zip(got, ref):
+        assert np.array_equal(a_, b_, equal_nan=True)
+    assert np.array_equal(np.sort(lst), np.arange(B))
+    it = ref[4]  # (status, iter, rho of the first step)
+    pos = np.empty(B, dtype=np.int64)
+    pos[lst] = np.arange(B)
+    assert np.median(pos[it >= np.percentile(it, 95)]) < 0.35 * B
