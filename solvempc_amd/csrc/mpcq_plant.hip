@@ -343,6 +343,10 @@ __device__ __forceinline__ bool gj_rows(double (&row)[NC], double *piv, int n, i
         const double ip = 1.0 / pk;
         if (!(pk > 0.0)) ok = false;
         const double f = row[k];
+        // every lane runs the elimination (one multiply and one FMA per element); the pivot lane (one per
+        // plant) then overwrites its row with the scaled pivot row it keeps from the products, in a branch
+        // of its own instead of a 64-bit select per element on every lane
+        double t[NC];
 #pragma unroll
         for (int j = 0; j < NC; j += 2) {
             const double2 m2 = *(const double2 *)(piv + j);
@@ -350,11 +354,13 @@ __device__ __forceinline__ bool gj_rows(double (&row)[NC], double *piv, int n, i
 #pragma unroll
             for (int e = 0; e < 2; e++) {
                 const int jj = j + e;
-                double v;
-                if (r == k) v = (jj == k) ? ip : mk[e] * ip;
-                else v = (jj == k) ? -f * ip : row[jj] - f * (mk[e] * ip);
-                row[jj] = v;
+                t[jj] = mk[e] * ip;
+                row[jj] = (jj == k) ? -f * ip : row[jj] - f * t[jj];
             }
+        }
+        if (r == k) {
+#pragma unroll
+            for (int jj = 0; jj < NC; jj++) row[jj] = (jj == k) ? ip : t[jj];
         }
         wave_sync();
     }
