@@ -185,10 +185,11 @@ int mpcq_mpc_run_device(mpcq_ctx *ctx, double *X_dev, double *U_dev, double xref
 #define MPCQ_STREAM_WAVE 1
 #define MPCQ_STREAM_TILE 2
 int mpcq_get_stream_path(mpcq_ctx *ctx, int *kind);
-/* Hardest-first order of the last solve (benchmarks and tests): *ordered = 1 when it was
- * a tile-path MPC step run in ascending |max_j (A x_u - u)_j| (x_u = -P^-1 q, the QP's unconstrained
+/* Hardest-first order of the last solve (benchmarks and tests): *ordered = 1 when it
+ * was a tile-path MPC step or a one-pass distinct-plants step (mpcq_mpc_plants_step_device; the key from the
+ * batch's first plant) run in ascending |max_j (A x_u - u)_j| (x_u = -P^-1 q, the QP's unconstrained
  * optimum; binned 16 per octave), else 0; order (batch ints, or NULL) receives that step's QPs in the
- * order phase 0 ran them (synchronises).  The order changes no result. */
+ * order it ran them (synchronises).  The order changes no result. */
 int mpcq_get_order(mpcq_ctx *ctx, int *ordered, int *order);
 /* Per-QP counters of the last mpcq_mpc_run_device call (host arrays of `batch` ints, synchronises):
  * the ADMM iterations of all its control steps, and the steps whose solve did not end SOLVED
