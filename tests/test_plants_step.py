@@ -183,14 +183,14 @@ def test_full_config3_batch_every_plant(plant, dtype):
     print(f"fp32 config 3: {int(off.sum())} of {B} plants took a tie's other branch")
 
 
-@pytest.mark.parametrize("dtype", ["f32", "f64"])
-def test_hardest_first_plants_are_transparent(plant, dtype, monkeypatch):
+@pytest.mark.parametrize("dtype,N,B", [("f32", 20, 3001), ("f64", 20, 3001), ("f64", 32, 500), ("f64", 15, 777)])
+def test_hardest_first_plants_are_transparent(plant, dtype, N, B, monkeypatch):
     """The one-pass step runs its batch hardest-first (the first plant's order map, mpcq_api.cpp
     plants_order_map, and mpcq_order.hip's counting sort; slot i of the grid runs plant list[i]): every
     output bit-identical to index order (MPCQ_PLANT_ORDER=0) on a ragged batch, the list a permutation of
     it, and the plants that need the most iterations in its first part.  A second step with the same plant
-    arrays reuses the map (and the bin counters the first step's kernel cleared)."""
-    N, B = 20, 3001
+    arrays reuses the map (and the bin counters the first step's kernel cleared).  N = 32 fills the order's
+    64 map rows (m = 2N) and runs two plants per wave; N = 15 a short row per plant."""
     Ad, Bd, X, U = _plants(plant, B, 4)
 
     def run(order):
