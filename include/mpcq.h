@@ -49,7 +49,14 @@ extern "C" {
 
 /* ---- precision of the device iterate ------------------------------------------------------- */
 #define MPCQ_F64 0 /* fp64 throughout (the reference's precision)                            */
-#define MPCQ_F32 1 /* fp32 ADMM iterate, fp64 setup                                           */
+#define MPCQ_F32 1 /* fp32 ADMM iterate, fp64 setup.  Bound: where OSQP certifies primal
+                      infeasibility an fp32 iterate may not (the dual iterate of an infeasible QP
+                      grows without bound and its fp32 rounding moves the certificate's
+                      ||A' dy|| / ||dy|| past eps_prim_inf), and the QP then ends
+                      MPCQ_MAX_ITER_REACHED instead of MPCQ_PRIMAL_INFEASIBLE (never a solved
+                      status; osqp-eigen's solve() is false either way).  MPCQ_F64 and
+                      MPCQ_F64_MIXED return OSQP's status (tests/test_gpu.py
+                      test_infeasible_statuses_match_oracle)                                   */
 #define MPCQ_F64_MIXED 2 /* fp64 state, checks and solution; on the shared-plant tile path the plain
                             iterations before the last MPCQ_MIX_R of every check interval run in fp32
                             (MFMA f32 products), which the fp64 ones damp; every
@@ -78,7 +85,15 @@ typedef struct mpcq_dims {
 
 typedef struct mpcq_ctx mpcq_ctx;
 
-/* Device-resident views of a context's buffers (fp64, QP-major), for zero-copy callers. */
+/* Device-resident views of a context's buffers (fp64, QP-major), for zero-copy callers.
+ * The pointers never change, but the OUTPUTS (x, y, status, iter, rho) are published lazily on the
+ * shared-plant tile path: a solve leaves them in its warm state and they are formed
+ * from it when something reads them.  mpcq_device_view_get is such a read: the output arrays hold the
+ * last solve's values only after mpcq_device_view_get has been called AFTER that solve (call it again
+ * after every mpcq_solve / mpcq_mpc_step_device / graph replay), and they are written by kernels
+ * enqueued on the context's last stream (the stream of its last solve), so a reader on another stream
+ * must order itself after that stream (an event) or synchronise it.  A view fetched once and re-read
+ * after later solves shows an older solve's outputs.  The inputs (q, u, l) follow the same rule. */
 typedef struct mpcq_device_view {
     double *q;     /* batch*n   gradient (input of the next solve)      */
     double *u;     /* batch*m   upper bounds                            */
@@ -141,6 +156,7 @@ int mpcq_get_scaling(mpcq_ctx *ctx, double *D, double *E, double *c); /* plant 0
 #define MPCQ_PATH_LANE 2
 int mpcq_get_path(mpcq_ctx *ctx, int *kind, int *paired);
 
+/* Fill *view and publish the last solve's pending outputs into it (see mpcq_device_view above). */
 int mpcq_device_view_get(mpcq_ctx *ctx, mpcq_device_view *view);
 
 /* ---- condensed-MPC front end: ModelPredictiveControlAPI::controllerStep, batched ------------

@@ -725,10 +725,10 @@ int mpcq_cold_start(mpcq_ctx *c)
 
 int mpcq_warm_start(mpcq_ctx *c, const double *x, const double *y)
 {
-    c->xy_lazy = false;  // (x, y are staged in the output buffers below)
     int rc = check_ctx(c, kGeneric);
     if (rc) return rc;
     if (!x || (c->dims.m && !y)) return fail(MPCQ_ERR_ARG, "null x/y");
+    c->xy_lazy = false;  // (x, y are staged in the output buffers below; a rejected call keeps a pending x, y)
     // stage in the output buffers (overwritten by the next solve)
     if ((rc = h2d(c->d_x, x, 8 * (size_t)c->dims.batch * c->dims.n, c->last))) return rc;
     if ((rc = h2d(c->d_y, y, 8 * (size_t)c->dims.batch * c->dims.m, c->last))) return rc;
@@ -1857,14 +1857,22 @@ int mpcq_mpc_plants_step_device(mpcq_ctx *c, int nx, int s_rows, const double *A
 {
     int rc = check_generic_dims(c);
     if (rc) return rc;
-    if ((rc = materialize_xy(c)) || (rc = materialize_rho(c))) return rc;  // (a pending lazy x, y, rho first: the
-                                                                             // kernel below rewrites the state)
     const int n = c->dims.n, m = c->dims.m;
     if (nx <= 0 || nx > 8 || s_rows < 0) return fail(MPCQ_ERR_ARG, "plants_step: 1 <= nx <= 8, s_rows >= 0");
     if (m != 2 * n || n > 32) return fail(MPCQ_ERR_ARG, "plants_step: n = N <= 32, m = 2N (ModelPredictiveControlAPI.cpp:47-48)");
     if (c->dims.n_plants != c->dims.batch) return fail(MPCQ_ERR_ARG, "plants_step: one plant per QP (n_plants == batch)");
     if (!Ad || !Bd || !Cd || !K || !Q || !R || !RD || !X || !U) return fail(MPCQ_ERR_ARG, "plants_step: null array");
     hipStream_t s = (hipStream_t)stream;
+    // the kernel below rewrites x, y, rho, status and iter of every QP on `s`: a pending lazy publication of an
+    // earlier solve is dropped, not formed (it would be wasted work, and on another stream unordered with s)
+    c->xy_lazy = c->rho_lazy = c->info_lazy = false;
+    if (c->last && c->last != s) {  // (the earlier solve's work on its stream before this one's writes)
+        hipEvent_t ev;
+        HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        const hipError_t e1 = hipEventRecord(ev, c->last), e2 = e1 == hipSuccess ? hipStreamWaitEvent(s, ev, 0) : e1;
+        (void)hipEventDestroy(ev);
+        if (e2 != hipSuccess) return fail(MPCQ_ERR_HIP, "plants_step: stream ordering failed");
+    }
     HIPCHK(hipMemsetAsync(c->d_flags, 0, 4, s));
     mpcq::PlantStepArgs a{};
     a.n_plants = c->dims.batch;

@@ -160,7 +160,11 @@ template <typename T> __device__ __forceinline__ T ssum(T v, int lane)
 // apart), and the carry between a plant's row and its tail crosses rows by ds_bpermute (the LDS crossbar:
 // no VALU issue).  Lanes of no plant hold 0 in every scan input (their predicates are false), and lane 63
 // is the zero every other lane's carry reads; they count in plant 2's slot and take plant 2's reductions,
-// so their decisions (status, `done`) are plant 2's.
+// so their decisions (status, `done`) are plant 2's.  Lane 63 feeds every plant's carry, so the lanes of no
+// plant must hold exact, finite zeros whatever plant 2's data: they read a broadcast slot of their own (never
+// written: zero), their M^-1 rows are zeroed after the inverse and their K0 is 0, so x~, z~, y and w stay 0
+// on them even when plant 2 is non-finite (a NaN there would otherwise reach plants 0 and 1 through 0 * NaN).
+__device__ __forceinline__ bool lay3_noplant(int lane) { return (lane & 51) == 51; }
 __device__ __forceinline__ int lay3_plant(int lane) { return lane < 48 ? lane >> 4 : ((lane & 3) == 3 ? 2 : lane & 3); }
 __device__ __forceinline__ int lay3_row(int lane) { return lane < 48 ? lane & 15 : ((lane & 3) == 3 ? 32 : 16 + ((lane >> 2) & 3)); }
 template <int LAY> __device__ __forceinline__ int lay_plant(int lane) { return LAY == 3 ? lay3_plant(lane) : lane >> 5; }
@@ -376,8 +380,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     static_assert(LAY == 2 || (LAY == 3 && NC <= 20), "three plants per wave: N <= 20");
     using PL = PlantLds<NC>;
     __shared__ PL lds[LAY];
-    __shared__ __attribute__((aligned(16))) T bx[LAY][NC], bw[LAY][NC];  // per-plant broadcasts
+    // per-plant broadcasts; LAY 3: slot 3 belongs to the lanes of no plant and stays zero
+    constexpr int NB = LAY == 3 ? LAY + 1 : LAY;
+    __shared__ __attribute__((aligned(16))) T bx[NB][NC], bw[NB][NC];
     const int lane = threadIdx.x, h = lay_plant<LAY>(lane), r = lay_row<LAY>(lane);
+    const bool noplant = LAY == 3 && lay3_noplant(lane);
     const int slot = blockIdx.x * LAY + h;
     const bool live = slot < a.n_plants;
     // (hardest-first: the slot's plant from the order list, clamped to the batch like the tile kernel's)
@@ -388,7 +395,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     const int N = a.N, n = N, nx = a.nx;
     const bool lr = r < N;
     PL &S = lds[h];
-    T *bxh = bx[h], *bwh = bw[h];
+    T *bxh = bx[noplant ? NB - 1 : h], *bwh = bw[noplant ? NB - 1 : h];
     const SolverSettings &st = a.st;
     // cold-path views: lane indices re-derived opaquely, so the loop does not keep the addresses of
     // the refactorisation, the checks and the finalize live in VGPRs across the hot iteration
@@ -396,6 +403,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     if (r < NC) {  // broadcast slots beyond N stay zero (row_dot reads the whole capacity)
         bxh[r] = T(0);
         bwh[r] = T(0);
+    }
+    if (LAY == 3 && lane < NC) {
+        bx[NB - 1][lane] = T(0);
+        bw[NB - 1][lane] = T(0);
     }
 
     // ---------------------------------------------------------------- 1. condensing
@@ -615,6 +626,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
             row[j] = v;
         }
         const bool ok = gj_rows<NC>(row, S.piv(), n, r);
+        if (!lr) {  // (a row of no step: exact zeros, not 0 - 0 * t with t from a possibly non-finite pivot row)
+#pragma unroll
+            for (int j = 0; j < NC; j++) row[j] = 0.0;
+        }
         double g = 0.0, pre = 0.0;
 #pragma unroll
         for (int j = 0; j < NC; j += 2) {
@@ -636,6 +651,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
             }
         }
         gk = lr ? (T)(-g) : T(0);
+        if constexpr (!MERGED) {
+            if (!lr) {  // (D, E of a non-finite plant would make 0 * NaN here)
+#pragma unroll
+                for (int j = 0; j < NC; j++) Btc[j] = T(0);
+            }
+        }
         return ok;
     };
 
@@ -646,7 +667,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     // fp64 rho0, not (double)(float)rho0, so a rebuild its partner half triggers reproduces its bits)
     double rho_f = rho0;
     const T alpha = (T)st.alpha, oma = T(1) - (T)st.alpha;
-    const T ET = (T)(lr ? Er : 0.0), DT = (T)Dd, K0T = (T)K0;
+    const T ET = (T)(lr ? Er : 0.0), DT = (T)Dd, K0T = (T)(noplant ? 0.0 : K0);
     // (A^ x)_r = E_r K0 sum_{k<=r} D_k x_k: E_r K0 is formed in the loop from ET, K0T (one multiply,
     // where a hoisted copy was the 3-waves/SIMD allocation's spill reloaded every iteration)
     const T sigT = (T)st.sigma;

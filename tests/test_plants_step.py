@@ -223,3 +223,38 @@ def test_hardest_first_plants_are_transparent(plant, dtype, N, B, monkeypatch):
     pos[lst] = np.arange(B)
     if N == 20:  # (the bench horizon, where the ranking was measured: DESIGN.md §4.3b)
         assert np.median(pos[it >= np.percentile(it, 95)]) < 0.35 * B
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+@pytest.mark.parametrize("layout", ["3", "2"])
+@pytest.mark.parametrize("poison", ["X", "Ad"])
+def test_nonfinite_plant_stays_in_its_own_lanes(plant, dtype, layout, poison, monkeypatch):
+    """Every QP is independent, as in OSQP: a plant with a NaN state (X) or non-finite plant data (Ad) must
+    leave every other plant's results bit for bit unchanged.  In the three-plants-per-wave layout the lanes of
+    no plant (51, 55, 59, 63) belong to plant 2's slot and lane 63 is the zero every other plant's scan carry
+    reads, so slot 2 is poisoned: plants 0 and 1 of its wave must not see it (index order, so plant i runs in
+    slot i; then the hardest-first default, where the poisoned plant's key is NaN and sorts last)."""
+    N, B = 20, 7
+    Ad, Bd, X, U = _plants(plant, B, 6)
+    if layout == "2":
+        monkeypatch.setenv("MPCQ_PLANT_LAYOUT", "2")
+    Ad2, X2 = Ad.copy(), X.copy()
+    if poison == "X":
+        X2[2, 1] = np.nan
+    else:
+        Ad2[2, 0, 0] = np.inf
+    for order in ("0", None):
+        if order:
+            monkeypatch.setenv("MPCQ_PLANT_ORDER", order)
+        else:
+            monkeypatch.delenv("MPCQ_PLANT_ORDER", raising=False)
+        res = []
+        for a_, x_ in ((Ad, X), (Ad2, X2)):
+            s, Ug = _fused(plant, a_, Bd, x_, U, N, dtype)
+            res.append((s.solution(), s.dual(), Ug, *s.info()))
+            s.close()
+        ok = np.arange(B) != 2
+        for a_, b_ in zip(res[0], res[1]):
+            assert np.array_equal(a_[ok], b_[ok], equal_nan=True)
+        assert np.all(res[0][3] == sm.SOLVED)
+        assert res[1][3][2] != sm.SOLVED and res[1][2][2] == U[2]  # (no move applied to the poisoned plant)
