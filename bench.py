@@ -65,6 +65,11 @@ def parse(argv=None):
                         "(dist.strong_block); BASELINE config 3 is `--workload perplant --scaling strong`")
     p.add_argument("--global-batch", type=int, default=0,
                    help="strong scaling: QPs of the whole job (default: 1,048,576 for perplant, else --batch)")
+    p.add_argument("--cfg3-strong", type=int, default=1,
+                   help="cfg2 line: also run BASELINE config 3 as written -- ONE batch of --cfg3-global-batch "
+                        "randomised plants split over the N ranks, RCCL gather of U to rank 0 -- and report it as "
+                        "the line's `cfg3_strong` block (0 = skip)")
+    p.add_argument("--cfg3-global-batch", type=int, default=1 << 20, help="plants of the cfg3_strong job")
     p.add_argument("--ctrl-steps", type=int, default=1000, help="control steps per bench step (stream)")
     p.add_argument("--noise", type=float, default=1e-2, help="plant noise std (stream; SURVEY §8d: var 1e-4)")
     p.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
@@ -417,11 +422,27 @@ def main_dry(a, rank, world, dist):
                                                     "parallelism": f"dp{world}"})
     rec["dry_run"] = True
     rec["collective"] = _collective(dist, world, got)
-    full = np.concatenate([t.numpy()[:mdist.strong_block(total, r, world)[1] if a.scaling == "strong" else count]
-                           for r, t in enumerate(got)])
+    full = (mdist.unpad(got, total, world) if a.scaling == "strong" else torch.cat(got)).numpy()
     rec["collective"]["gathered"] = int(full.size)
     rec["collective"]["matches_stream"] = bool(np.array_equal(full, workload.mpc_states(a.seed, 0, total)[1]))
     return rec
+
+
+def cfg3_block(r3: dict) -> dict:
+    """The cfg2 line's `cfg3_strong` block: BASELINE config 3's job (one global batch of randomised plants split
+    over the ranks, condense + setup + one controllerStep each, U gathered to rank 0) from its own record."""
+    rl = r3.get("roofline") or {}
+    keep = ("value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "scaling", "dtype", "config", "iters",
+            "collective")
+    out = {k: r3[k] for k in keep if k in r3}
+    out["metric"] = "QP solves/sec (BASELINE config 3: 1 M randomised plants, n_x=4, n_u=1, N=20, sharded, RCCL gather)"
+    if rl:
+        out["roofline"] = {k: rl[k] for k in ("bound", "achieved", "peak", "unit", "frac", "kernel", "kernel_ms")
+                           if k in rl}
+        out["roofline"]["note"] = "rank 0's kernel time and plants (the ranks' blocks differ by at most one plant)"
+    if r3.get("dry_run"):
+        out["dry_run"] = True
+    return out
 
 
 # ----------------------------------------------------------------------------- main
@@ -452,6 +473,15 @@ def main():
             rec = main_quadrotor(a, rank, world, local, dist, torch.device("cuda", local))
         else:
             rec = main_lti(a, rank, world, local, dist, torch.device("cuda", local))
+        if a.workload == "cfg2" and a.cfg3_strong and a.scaling == "weak":
+            # BASELINE config 3 as written, in the same run (and so in the driver's multi-GPU SCALE lines)
+            a3 = parse(["--workload", "perplant", "--scaling", "strong", "--gpus", str(a.gpus),
+                        "--global-batch", str(a.cfg3_global_batch), "--steps", str(a.steps),
+                        "--warmup", str(min(a.warmup, 2)), "--cpu-seconds", "0", "--backend", a.backend])
+            rec3 = (main_dry(a3, rank, world, dist) if a.dry_run
+                    else main_lti(a3, rank, world, local, dist, torch.device("cuda", local)))
+            if rank == 0:
+                rec["cfg3_strong"] = cfg3_block(rec3)
         if rank == 0:
             print(json.dumps(rec))
     finally:
@@ -644,6 +674,8 @@ def main_lti(a, rank, world, local, dist, dev):
         rec["iters"]["stream_unsolved_steps"] = int(solver.stream_unsolved())
         rec["iters"]["final_max_abs_X"] = float(X_d.abs().max().item())
     rec["collective"] = _collective(dist, world, got)
+    if a.scaling == "strong":  # (the blocks are padded to the longest for the equal-size gather)
+        rec["collective"]["gathered"] = int(mdist.unpad(got, total, world).numel()) if world > 1 else B
     if perplant:
         # One kernel per step: condensing + Ruiz + KKT inverse (fp64) and the ADMM (T = dtype) of every
         # plant, two plants per wave.  FLOPs as the kernel performs them (workload.flops_plant_step;

@@ -27,6 +27,14 @@ def strong_block(total: int, rank: int, world: int) -> tuple[int, int]:
     return start, base + (1 if rank < rem else 0)
 
 
+def unpad(gathered, total: int, world: int):
+    """Rank 0's gathered blocks of a strong-scaling job (each padded to the longest block for the equal-size
+    gather) trimmed and joined: the moves of global QPs 0 .. total - 1 in order."""
+    import torch
+
+    return torch.cat([t[:strong_block(total, r, world)[1]] for r, t in enumerate(gathered)])
+
+
 def gather_moves(dist, moves, world: int, rank: int, gathered=None):
     """Gather every rank's applied moves to rank 0 (``dist.gather``; equal block sizes).  Returns the
     list of per-rank tensors on rank 0 and None elsewhere."""

@@ -85,7 +85,23 @@ def stream_states(seed: int, start: int, count: int):
 def randomized_plants(plant: dict, seed: int, start: int, count: int, rel: float = 0.02, attempts: int = 64):
     """Config 3 plants for global indices start .. start+count-1: Ad = Ad0 o (1 + rel eps),
     Bd = Bd0 o (1 + rel eps), eps ~ N(0, 1) (Box-Muller on draws 32a .. 32a+19 of attempt a); a draw
-    with spectral radius rho(Ad) >= 1 is rejected and redrawn (after `attempts` the nominal plant)."""
+    with spectral radius rho(Ad) >= 1 is rejected and redrawn (after `attempts` the nominal plant).
+    A plant depends on its global index only, so large batches run as index blocks on a thread pool
+    (numpy and LAPACK release the GIL): the same arrays as one block."""
+    import os
+    from concurrent.futures import ThreadPoolExecutor
+
+    workers = min(16, os.cpu_count() or 1, max(1, count // 16384))
+    if workers <= 1:
+        return _randomized_block(plant, seed, start, count, rel, attempts)
+    base, rem = divmod(count, workers)
+    blocks = [(start + w * base + min(w, rem), base + (1 if w < rem else 0)) for w in range(workers)]
+    with ThreadPoolExecutor(workers) as ex:
+        parts = list(ex.map(lambda b: _randomized_block(plant, seed, b[0], b[1], rel, attempts), blocks))
+    return np.concatenate([p_[0] for p_ in parts]), np.concatenate([p_[1] for p_ in parts])
+
+
+def _randomized_block(plant: dict, seed: int, start: int, count: int, rel: float, attempts: int):
     Ad0, Bd0 = np.asarray(plant["Ad"], dtype=np.float64), np.asarray(plant["Bd"], dtype=np.float64)
     nx = Ad0.shape[0]
     k = nx * nx + nx

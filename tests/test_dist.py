@@ -40,6 +40,31 @@ def _worker(rank, port, out):
     dist.destroy_process_group()
 
 
+def _plant_moves(start, count):
+    """BASELINE config 3 for global plants start .. start+count-1: each plant's ctor + one controllerStep
+    (oracle.plants_step, the per-rank solver here), the applied U."""
+    plant = workload.reference_plant()
+    Ad, Bd = workload.randomized_plants(plant, 2, start, count)
+    X, U = workload.mpc_states(2, start, count)
+    return oracle.plants_step(plant, Ad, Bd, X, U, N, nthreads=1)[0]
+
+
+def _strong_worker(rank, port, out, total):
+    """One rank of the cfg3_strong job: its strong block, padded to the longest block, gathered, trimmed."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD))
+    r, w, _ = mdist.world_from_env()
+    dist.init_process_group("gloo", rank=r, world_size=w)
+    start, count = mdist.strong_block(total, r, w)
+    pad = -(-total // w)
+    moves = torch.zeros(pad, dtype=torch.float64)
+    moves[:count] = torch.from_numpy(_plant_moves(start, count))
+    got = mdist.gather_moves(dist, moves, w, r)
+    if r == 0:
+        out.put(mdist.unpad(got, total, w).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -58,6 +83,24 @@ def test_two_rank_gather_equals_single_process():
         p.join(timeout=60)
         assert p.exitcode == 0
     np.testing.assert_array_equal(res, _moves(0, PER_RANK * WORLD))
+
+
+def test_strong_config3_gather_equals_single_process():
+    """bench.py's cfg3_strong job on 2 gloo ranks: ONE global batch of randomised plants (an odd count, so the
+    blocks differ by one and the gather pads), each rank solving its block; rank 0's gathered U, trimmed
+    (dist.unpad), equals the single-process result for the whole batch."""
+    total = 67
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_strong_worker, args=(r, port, q, total)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(res, _plant_moves(0, total))
 
 
 def test_blocks_tile_the_stream():
@@ -80,7 +123,7 @@ def test_bench_launches_its_own_ranks():
     root = Path(__file__).resolve().parents[1]
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
     r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2", "--backend", "gloo", "--dry-run",
-                        "--steps", "3", "--warmup", "1", "--batch", "1000"],
+                        "--steps", "3", "--warmup", "1", "--batch", "1000", "--cfg3-global-batch", "1001"],
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -89,6 +132,10 @@ def test_bench_launches_its_own_ranks():
     assert rec["n_gpus"] == 2 and rec["steps"] == 3 and rec["dry_run"] is True
     assert rec["collective"] == {"backend": "gloo", "world_size": 2, "gathered": 2000, "matches_stream": True}
     assert rec["scaling"] == "weak"
+    # the same line carries BASELINE config 3 as written: one global batch split over the two ranks
+    c3 = rec["cfg3_strong"]
+    assert c3["scaling"] == "strong" and c3["n_gpus"] == 2 and c3["config"]["global_batch"] == 1001
+    assert c3["collective"] == {"backend": "gloo", "world_size": 2, "gathered": 1001, "matches_stream": True}
 
 
 def test_bench_strong_scaling_splits_one_global_batch():
