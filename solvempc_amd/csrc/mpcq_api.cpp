@@ -1909,8 +1909,26 @@ int mpcq_mpc_plants_step_device(mpcq_ctx *c, int nx, int s_rows, const double *A
         a.order = list;
         a.ord_zero = cnt;
     }
+    const char *pst = debug_hook("MPCQ_PLANT_STAMPS");  // per-wave stage stamps (a -DMPCQ_PLANT_STAMPS build)
+    const size_t nwaves = (size_t)c->dims.batch;  // (an upper bound on the grid)
+    if (pst && *pst) {
+        if (c->d_stamps) (void)hipFree(c->d_stamps);
+        c->d_stamps = nullptr;
+        if (hipMalloc((void **)&c->d_stamps, 8 * 16 * nwaves) != hipSuccess) return fail(MPCQ_ERR_HIP, "hipMalloc failed (stamps)");
+        HIPCHK(hipMemsetAsync(c->d_stamps, 0, 8 * 16 * nwaves, s));
+        a.stamps = c->d_stamps;
+    }
     const int lr = mpcq_internal_plant_step_launch(&a, c->dims.dtype == MPCQ_F32, s);
     if (lr) return fail(lr == -1 ? MPCQ_ERR_ARG : MPCQ_ERR_HIP, "plants_step kernel launch failed");
+    if (pst && *pst) {
+        std::vector<long long> h(16 * nwaves);
+        HIPCHK(hipMemcpyAsync(h.data(), c->d_stamps, 8 * h.size(), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (FILE *f = std::fopen(pst, "wb")) {
+            std::fwrite(h.data(), 8, h.size(), f);
+            std::fclose(f);
+        }
+    }
     if (ordered) c->ord_clean = true;
     c->ord_last = ordered;
     c->mode = mpcq_ctx::Mode::OneShot;  // results only: no operator blocks were written

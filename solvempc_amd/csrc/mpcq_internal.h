@@ -391,6 +391,7 @@ struct PlantStepArgs {
     // zeroes the OrderBins::kBins counters ord_zero for the next sort
     const int *order;
     int *ord_zero;
+    long long *stamps;  // debug builds (-DMPCQ_PLANT_STAMPS): 16 per wave, stage clock stamps
 };
 }  // namespace mpcq
 

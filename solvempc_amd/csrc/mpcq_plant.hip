@@ -371,6 +371,19 @@ __device__ __forceinline__ bool gj_rows(double (&row)[NC], double *piv, int n, i
     return ok;
 }
 
+// Stage clock stamps of a debug build (-DMPCQ_PLANT_STAMPS, tools/plant_stamps.py): 16 per wave
+#ifdef MPCQ_PLANT_STAMPS
+#define MPCQ_PSTAMP(k, v)                                                              \
+    do {                                                                               \
+        if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 16 + (k)] = (v); \
+    } while (0)
+#else
+#define MPCQ_PSTAMP(k, v) \
+    do {                  \
+    } while (0)
+#endif
+#define MPCQ_PTIME(k) MPCQ_PSTAMP(k, (long long)__builtin_amdgcn_s_memtime())
+
 // WPE: waves per SIMD the register allocation is held to (2, or 3 for A/B: MPCQ_PLANT_WPE); LAY: plants per
 // wave (2: one per 32-lane half; 3: N <= 20, rows plus interleaved tails, see lay3_*)
 template <typename T, int NC, int WPE, int LAY>
@@ -392,6 +405,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     const int p = plant;  // a dead half runs plant 0's data and publishes nothing
     if (blockIdx.x == 0 && a.ord_zero)  // the order's bin counters, read by its finished sort: the next sort's
         for (int i = threadIdx.x; i < OrderBins::kBins; i += 64) a.ord_zero[i] = 0;
+    MPCQ_PTIME(0);
     const int N = a.N, n = N, nx = a.nx;
     const bool lr = r < N;
     PL &S = lds[h];
@@ -440,6 +454,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
             }
             wave_sync();
         }
+        MPCQ_PTIME(1);
         double cab = 0.0;  // Cd Ad^r Bd
         if (lr) {
 #pragma unroll
@@ -509,6 +524,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     for (int c = 0; c < 8; c++)
         if (c < nx) kx += K[c] * Xv[c];
 
+    MPCQ_PTIME(2);
     // ---------------------------------------------------------------- 2. scale_data (Ruiz)
     // setup_inv_kernel's arithmetic with A structural: the top half of Gbar is K0 L (L lower-triangular
     // ones, :332-347) and the bottom half its negation, so A^ = E K0 L D entrywise, its column norms are
@@ -559,6 +575,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         if (r < NC) S.SE()[r] = se;
     }
 
+    MPCQ_PTIME(3);
     // ---------------------------------------------------------------- 3. controllerStep front end
     T qh = T(0), ut = T(kInfty), ub = T(kInfty);
     double qs = 0.0, up_t = 0.0, up_b = 0.0;
@@ -660,6 +677,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         return ok;
     };
 
+    MPCQ_PTIME(4);
     const double rho0 = fmin(fmax(st.rho, kRhoMin), kRhoMax);
     T xs = T(0), zt = T(0), zb = T(0), yt = T(0), yb = T(0);
     T rho = (T)rho0, rinv = T(1) / rho;
@@ -722,6 +740,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
                          // half at its own rho_f; a half whose rho did not move rebuilds the same bits)
             const bool ok = factor(rho_f);
             refactor = false;
+            MPCQ_PSTAMP(first ? 5 : 10, first ? (long long)__builtin_amdgcn_s_memtime() : (long long)it);
             if (first) {
                 first = false;
                 setup_ok = ok;
@@ -780,7 +799,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
             yb = tt_fma(rho, v - zn, yb);
             zb = zn;
         }
+        if (it == 1) MPCQ_PTIME(6);
         if (!info) continue;
+        if (it == ct) MPCQ_PTIME(7);
 
         // ---- update_info: residuals, norms, certificates and the rho estimate in fp64 from the T
         // iterate (exact in fp64), so an fp32 kernel takes OSQP's decisions on the same numbers as an
@@ -908,14 +929,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
             const int s2 = check_termination(true);
             if (!done && !term) { status = s2 != kUnsolved ? s2 : kMaxIterReached; term = true; }
         }
+        if (it == ct) MPCQ_PTIME(8);
         refactor = wave_any(refactor);  // uniform (the other half rebuilds its own M at its own rho)
         if (term) {
             finalize();
             done = true;
         }
     }
+    MPCQ_PTIME(9);
+    MPCQ_PSTAMP(11, (long long)it);
     if (threadIdx.x == 0 && !wave_all(setup_ok || !live)) atomicOr(a.flags, 1);
 }
+#undef MPCQ_PTIME
+#undef MPCQ_PSTAMP
 
 template <typename T, int NC, int LAY>
 int plant_step_launch_l(const PlantStepArgs &a, hipStream_t s)
