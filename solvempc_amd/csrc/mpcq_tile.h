@@ -1242,6 +1242,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
         }
     };
     MPCQ_TSTAMP(2, (long long)__builtin_amdgcn_s_memtime());
+    // MIX: the wave runs every remaining iteration in fp64 once one of its running columns looks primal
+    // infeasible (OSQP's certificate candidate, u' dy < eps ||dy||, with ||A' dy|| within 1e4 eps ||dy|| but not
+    // below eps ||dy||): an infeasible QP's dual iterate grows without bound, the fp32 stretches' rounding of it
+    // keeps ||A' dy|| / ||dy|| near 1e-4 .. 1e-2 where fp64 reaches ~1e-12, and the certificate would then be
+    // missed (the QP running to max_iter).  Feasible QPs' candidates sit at ratios >= ~40 (config 2), so the
+    // switch does not fire on them.  Wave-uniform.
+    bool mix64 = false;
     while (!all_done()) {
         if constexpr (PAIRED) {
             // plain iterations up to the next info iteration, with the operators held in VGPRs
@@ -1257,7 +1264,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
 #ifdef MPCQ_MIX_STAMPS  // debug build: cycles in the fp32 stretches -> phase stamp 5
                 const long long t_mix = a.stamps ? (long long)__builtin_amdgcn_s_memtime() : 0;
 #endif
-                if (it < n32) {
+                if (it < n32 && !mix64) {
                     float xs32[G][NS], z32[G][MS], y32[G][MS], uh32[G][MS], gv32[G][NS], rho32[G], adk32[G][KNR];
 #pragma unroll
                     for (int gi = 0; gi < G; gi++) {
@@ -1635,6 +1642,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 tile_mv_g<T, G, NT, KM, KMP>(img + L.AhT, d, atd, lane, nullptr);
             }
             const T *Dinv = fresh_ptr((const T *)s_Dinv);
+            bool near = false;
 #pragma unroll
             for (int gi = 0; gi < G; gi++) {
                 T nat = 0;
@@ -1642,6 +1650,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 for (int s = 0; s < KN; s++) nat = nrm(nat, scaled_term ? atd[gi][s] : Dinv[4 * s + g] * atd[gi][s]);
                 nat = col_max(nat);
                 res[gi] = cand[gi] && nat < eps * ndy[gi];
+                if constexpr (MIX) near = near || (cand[gi] && !res[gi] && nat < T(1e4) * eps * ndy[gi]);
+            }
+            if constexpr (MIX) {
+                if (wave_any(near)) mix64 = true;
             }
         };
         // OSQP is_dual_infeasible on delta_x^ = W dx, per group.
