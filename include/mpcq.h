@@ -52,11 +52,11 @@ extern "C" {
 #define MPCQ_F32 1 /* fp32 ADMM iterate, fp64 setup.  Bound: where OSQP certifies primal
                       infeasibility an fp32 iterate may not (the dual iterate of an infeasible QP
                       grows without bound and its fp32 rounding moves the certificate's
-                      ||A' dy|| / ||dy|| past eps_prim_inf), and the QP then ends
-                      MPCQ_MAX_ITER_REACHED instead of MPCQ_PRIMAL_INFEASIBLE (never a solved
-                      status; osqp-eigen's solve() is false either way).  MPCQ_F64 and
-                      MPCQ_F64_MIXED return OSQP's status (tests/test_gpu.py
-                      test_infeasible_statuses_match_oracle)                                   */
+                      ||A' dy|| / ||dy|| past eps_prim_inf), and the QP then runs to max_iter:
+                      MPCQ_MAX_ITER_REACHED, or MPCQ_SOLVED_INACCURATE where OSQP's approximate
+                      check passes there, instead of MPCQ_PRIMAL_INFEASIBLE (never MPCQ_SOLVED;
+                      osqp-eigen's solve() is false either way).  MPCQ_F64 and MPCQ_F64_MIXED
+                      return OSQP's status (tests/test_gpu.py test_infeasible_statuses_match_oracle) */
 #define MPCQ_F64_MIXED 2 /* fp64 state, checks and solution; on the shared-plant tile path the plain
                             iterations before the last MPCQ_MIX_R of every check interval run in fp32
                             (MFMA f32 products), which the fp64 ones damp; every
