@@ -367,7 +367,7 @@ def _timed_loop(a, step, dist, world, dev):
 
 def traffic_per_solve(name, batch, N):
     """HBM bytes of one bench step of the dominant kernel from the committed PMC pass of the same bench
-    command (tools/gpu_r05.sh pmc:<workload>,<dtype> -> tools/pmc_traffic.py -> profiles/pmc_traffic_<name>.json),
+    command (tools/gpu.sh pmc:<workload>,<dtype> -> tools/pmc_traffic.py -> profiles/pmc_traffic_<name>.json),
     or None when no pass of this batch and horizon is committed."""
     f = ROOT / "profiles" / f"pmc_traffic_{name}.json"
     try:

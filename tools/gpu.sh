@@ -1,6 +1,6 @@
 #!/bin/bash
-# One GPU call of round 5: the GPU test suite, the default bench line and optional extras, each step under its
-# own time limit, stopping at the first failure.  Usage: tools/gpu_r05.sh TAG [steps...]
+# One GPU call: the GPU test suite, the default bench line and optional extras, each step under its
+# own time limit, stopping at the first failure.  Usage: tools/gpu.sh TAG [steps...]
 #   steps: tests | tests:<pytest -k expr> | bench | bench:<args> | probe:<dtype> | smoke | prof | pmc:<counters>
 #          | envbench:VAR=val,<args> | pmcw:VAR=val,<dtype> | stamps:mimo_setup | tstamps:<dtype> | calib
 set -o pipefail
@@ -15,6 +15,12 @@ for step in "$@"; do
       if [ -n "$arg" ]; then k=(-k "$arg"); else k=(); fi
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${k[@]}" \
         > "$out/tests.log" 2>&1 || { echo "tests failed"; tail -30 "$out/tests.log"; exit 1; } ;;
+    testsk)  # as tests, but failed assertions (pytest exit 1) do not end the call; any other failure does
+      if [ -n "$arg" ]; then k=(-k "$arg"); else k=(); fi
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread "${k[@]}" \
+        > "$out/tests.log" 2>&1; rc=$?
+      [ $rc -eq 0 ] || [ $rc -eq 1 ] || { echo "tests crashed rc=$rc"; tail -30 "$out/tests.log"; exit 1; }
+      grep -E "^(FAILED|ERROR)|passed|failed" "$out/tests.log" | tail -12 ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 \
         || { echo "smoke failed"; tail -20 "$out/smoke.log"; exit 1; } ;;

@@ -1,5 +1,5 @@
 """HBM traffic per launch of a bench workload's dominant kernel from a tools/pmc.sh FETCH_SIZE / WRITE_SIZE
-run (dev tool; tools/gpu_r05.sh step pmc:<workload>,<dtype>).
+run (dev tool; tools/gpu.sh step pmc:<workload>,<dtype>).
 
 Sums each counter over the dispatches of every kernel whose name contains one of the given substrings,
 divides by the number of bench steps the run made (warmup + steps), and writes
