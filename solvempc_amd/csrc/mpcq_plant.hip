@@ -329,8 +329,11 @@ template <int NC> struct PlantLds {
 };
 
 // Gauss-Jordan inverse of this half's SPD matrix (n x n; SPD: no pivoting), lane r holding row r in
-// registers.  Per pivot the owner publishes its row through LDS (one wave: the DS queue keeps the
-// order, wave_sync only pins the compiler's); every lane then updates its row in place.
+// registers.  Per pivot the owner publishes its row p through LDS (one wave: the DS queue keeps the
+// order, wave_sync only pins the compiler's); then every lane updates its row in place without a branch:
+// row <- fma(-g, p, s row) with (s, g) = (1, row[k] / p[k]) on the other rows and (1 / p[k], 0) on the
+// pivot row (a multiply by 1 and an fma with 0 are exact), and element k <- -g, or 1 / p[k] on the pivot
+// row.  Two VALU per element per pivot.
 template <int NC>
 __device__ __forceinline__ bool gj_rows(double (&row)[NC], double *piv, int n, int r)
 {
@@ -346,11 +349,8 @@ __device__ __forceinline__ bool gj_rows(double (&row)[NC], double *piv, int n, i
         const double pk = piv[k];
         const double ip = 1.0 / pk;
         if (!(pk > 0.0)) ok = false;
-        const double f = row[k];
-        // every lane runs the elimination (one multiply and one FMA per element); the pivot lane (one per
-        // plant) then overwrites its row with the scaled pivot row it keeps from the products, in a branch
-        // of its own instead of a 64-bit select per element on every lane
-        double t[NC];
+        const bool pr = r == k;
+        const double sc = pr ? ip : 1.0, g = pr ? 0.0 : row[k] * ip;
 #pragma unroll
         for (int j = 0; j < NC; j += 2) {
             const double2 m2 = *(const double2 *)(piv + j);
@@ -358,13 +358,8 @@ __device__ __forceinline__ bool gj_rows(double (&row)[NC], double *piv, int n, i
 #pragma unroll
             for (int e = 0; e < 2; e++) {
                 const int jj = j + e;
-                t[jj] = mk[e] * ip;
-                row[jj] = (jj == k) ? -f * ip : row[jj] - f * t[jj];
+                row[jj] = (jj == k) ? (pr ? ip : -g) : fma(-g, mk[e], row[jj] * sc);
             }
-        }
-        if (r == k) {
-#pragma unroll
-            for (int jj = 0; jj < NC; jj++) row[jj] = (jj == k) ? ip : t[jj];
         }
         wave_sync();
     }
@@ -440,6 +435,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
             Cr[r] = r < nx ? Cd[r] : 0.0;
         }
         wave_sync();
+        MPCQ_PTIME(12);
         for (int k = 0; k < N; k++) {
             double v = 0.0, c = 0.0;
 #pragma unroll
@@ -463,6 +459,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         const double cs = l_psum<LAY>(cab, lane);  // Su(i, j) = CS[i - j] = sum_{k <= i - j} CAB[k]
         if (r < NC) S.CS[r] = lr ? cs : 0.0;
         wave_sync();
+        MPCQ_PTIME(13);
     }
     const double Q = a.Q[p], R = a.R[p], RD = a.RD[p];
     const double *K = a.K + (size_t)p * nx;
@@ -502,6 +499,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         }
     }
     wave_sync();
+    MPCQ_PTIME(14);
     double pr[NC];
 #pragma unroll
     for (int j = 0; j < NC; j++) {
@@ -516,7 +514,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     if (lr) {
         const double Fu = 2.0 * (R + Q * G[PL::pk(r, N - 1)]);  // Fu[r] (:305, incl. the diagonal() quirk: R 1)
         double f = 0.0;
-        for (int k = r; k < N; k++) f += S.CS[k - r] * (S.tmp[k] - a.xref);
+        const double xr = a.xref;
+#pragma unroll
+        for (int kk = 0; kk < NC; kk++)  // k = r + kk (fixed trip count: the LDS reads issue together)
+            if (r + kk < N) f += S.CS[kk] * (S.tmp[r + kk < NC ? r + kk : NC - 1] - xr);
         qk = (2.0 * Q) * f + Fu * Uv;
     }
     double kx = 0.0;  // K X (Sbar rows < s_rows, :185,208)
@@ -535,9 +536,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     double Dr = lr ? 1.0 : 0.0, Er = lr ? 1.0 : 0.0;  // (0 on dead lanes: neutral in every scan)
     double cost = 1.0, cp = 1.0;
     for (int it = 0; it < st.scaling; it++) {
-        double vp = 0.0;
+        double vq[4] = {0.0, 0.0, 0.0, 0.0};  // (max is exact in any order: four short chains)
 #pragma unroll
-        for (int j = 0; j < NC; j++) vp = hwmax_abs(vp, pr[j]);
+        for (int j = 0; j < NC; j++) vq[j & 3] = hwmax_abs(vq[j & 3], pr[j]);
+        const double vp = hwmax(hwmax(vq[0], vq[1]), hwmax(vq[2], vq[3]));
         const double emax = l_suffix_max<LAY>(Er, lane), dpre = l_prefix_max<LAY>(Dr, lane);
         const double va = (aK0 * Dr) * emax, ve = (aK0 * Er) * dpre;
         const double dt = 1.0 / sqrt(limit_scaling_p(fmax(cp * vp, va)));
@@ -598,7 +600,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         // |q^| in both scalings: q does not change during the solve, so every check reads these (the check's
         // own arithmetic: DiD = 1 / D_r, the max over the plant's steps)
         const double qd = (double)qh, DiD = 1.0 / (lr ? Dr : 1.0);
-        const double qn_r = l_max<LAY>(lr ? fabs(qd) : 0.0, lane), qn_s = l_max<LAY>(lr ? fabs(DiD * qd) : 0.0, lane);
+        const double qn_r = hwmax(l_max<LAY>(lr ? fabs(qd) : 0.0, lane), 0.0);  // (0 and NaN: as pmax below)
+        const double qn_s = hwmax(l_max<LAY>(lr ? fabs(DiD * qd) : 0.0, lane), 0.0);
         if (r == 0) {
             S.sh[0] = cost;
             S.sh[1] = cinv;
@@ -838,7 +841,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
             pxn_r = fabs(px);
             pxn_s = fabs(DiD * px);
         }
-        auto pmax = [&](TD v) { return l_max<LAY>(v, lane); };
+        // (OSQP's vec_norm_inf starts from 0 and skips NaN: v_max with 0 returns the non-NaN operand, so a
+        // plant whose lanes are all NaN reads 0 in either layout, as OSQP does; the identity on finite norms)
+        auto pmax = [&](TD v) { return hwmax(l_max<LAY>(v, lane), 0.0); };
         // the norms in the scaling the termination test reads (scaled_termination: OSQP's scaled residuals,
         // else the unscaled ones), and the scaled ones adapt_rho reads: only the sets this iteration uses
         // (wave-uniform; with the default intervals three checks in four test termination only)

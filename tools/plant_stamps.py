@@ -2,7 +2,7 @@
 `SRC=mpcq_plant.hip DBGDIR=tools/dbg_r06p bash tools/build_dbg.sh MPCQ_PLANT_STAMPS`, run with
 MPCQ_LIBRARY=tools/dbg_r06p/libmpcq.so.  Runs the bench's batch (131,072 plants, seed 2, fp64, hardest-first)
 twice and prints the median shader cycles of each stage per wave (three plants) and the wave lifetimes.
-Stamps: 0 entry, 1 condensing recurrences, 2 lag table + P + q, 3 Ruiz, 4 front end, 5 first KKT inverse,
+Stamps: 0 entry, 1 condensing recurrences, 2 lag table + P + q (12 plant data, 13 CS scan, 14 lag table), 3 Ruiz, 4 front end, 5 first KKT inverse,
 6 iteration 1, 7 iteration ct (before its check), 8 its check, 9 exit; 11 the wave's last iteration.
 usage: python tools/plant_stamps.py [plants] [dtype]"""
 import os
@@ -37,10 +37,10 @@ torch.cuda.synchronize()
 h = np.fromfile(out, dtype=np.int64).reshape(-1, 16)
 h = h[h[:, 0] != 0]
 print(f"waves {len(h)} ({dtype}, {B} plants)")
-names = {1: "condensing recurrences", 2: "lag table, P, q", 3: "Ruiz", 4: "front end", 5: "first KKT inverse",
+names = {12: "plant data loads", 1: "condensing recurrences", 13: "CS scan", 14: "lag table", 2: "P, q", 3: "Ruiz", 4: "front end", 5: "first KKT inverse",
          6: "iteration 1", 7: "iterations 2 .. ct", 8: "check at ct", 9: "rest of the solve"}
 prev = h[:, 0]
-for k in range(1, 10):
+for k in (12, 1, 13, 14, 2, 3, 4, 5, 6, 7, 8, 9):
     d = h[:, k] - prev
     print(f"  {k} {names[k]:24s} median {np.median(d):9.0f}  mean {d.mean():9.0f}  p90 {np.percentile(d, 90):9.0f}")
     prev = h[:, k]
