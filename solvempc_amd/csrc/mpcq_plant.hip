@@ -295,7 +295,7 @@ template <int LAY> __device__ __forceinline__ bool l_any(bool p, int lane)  // a
 // the vectors Dv .. piv, each written once what it overlaps is dead.
 template <int NC> struct PlantLds {
     static constexpr int NP = NC * (NC + 1) / 2;
-    static constexpr int NU = (NC + 1) * 16 > NP + 7 * NC ? (NC + 1) * 16 : NP + 7 * NC;
+    static constexpr int NU = (NC + 1) * 16 > NP + 9 * NC ? (NC + 1) * 16 : NP + 9 * NC;
     static_assert(NP % 2 == 0, "16-B aligned vectors");
     double u[NU];
     double CS[NC], tmp[NC];
@@ -311,6 +311,10 @@ template <int NC> struct PlantLds {
     __device__ double *Ut() { return u + NP + 4 * NC; }
     __device__ double *Ub() { return u + NP + 5 * NC; }
     __device__ double *piv() { return u + NP + 6 * NC; }
+    __device__ double *Ei() { return u + NP + 7 * NC; }  // 1 / E, 1 / D (OSQP's Einv, Dinv; 1 beyond N)
+    __device__ double *Di() { return u + NP + 8 * NC; }
+    __device__ const double *Ei() const { return u + NP + 7 * NC; }
+    __device__ const double *Di() const { return u + NP + 8 * NC; }
     __device__ const double *Dv() const { return u + NP; }
     __device__ const double *Ev() const { return u + NP + NC; }
     __device__ const double *qh() const { return u + NP + 3 * NC; }
@@ -347,7 +351,11 @@ __device__ __forceinline__ bool gj_rows(double (&row)[NC], double *piv, int n, i
         }
         wave_sync();
         const double pk = piv[k];
-        const double ip = 1.0 / pk;
+        // 1 / pk by v_rcp_f64 and two Newton steps (within an ulp; the inverse is compared with the oracle's
+        // LDL solve at tolerance, not bitwise): five VALU where the IEEE division takes ten
+        double ip = __builtin_amdgcn_rcp(pk);
+        ip = fma(ip, fma(-pk, ip, 1.0), ip);
+        ip = fma(ip, fma(-pk, ip, 1.0), ip);
         if (!(pk > 0.0)) ok = false;
         const bool pr = r == k;
         const double sc = pr ? ip : 1.0, g = pr ? 0.0 : row[k] * ip;
@@ -437,12 +445,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         wave_sync();
         MPCQ_PTIME(12);
         for (int k = 0; k < N; k++) {
-            double v = 0.0, c = 0.0;
+            // (two FMA chains per product: the step's latency is the LDS round trip plus four FMAs)
+            double v0 = 0.0, v1 = 0.0, c0 = 0.0, c1 = 0.0;
 #pragma unroll
-            for (int s = 0; s < 8; s++) {
-                v += adr[s] * V[k * 8 + s];
-                c += Cr[k * 8 + s] * adc[s];
+            for (int s = 0; s < 8; s += 2) {
+                v0 = fma(adr[s], V[k * 8 + s], v0);
+                v1 = fma(adr[s + 1], V[k * 8 + s + 1], v1);
+                c0 = fma(Cr[k * 8 + s], adc[s], c0);
+                c1 = fma(Cr[k * 8 + s + 1], adc[s + 1], c1);
             }
+            const double v = v0 + v1, c = c0 + c1;
             wave_sync();
             if (r < 8) {
                 V[(k + 1) * 8 + r] = v;
@@ -547,12 +559,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         if (r < NC) S.tmp[r] = lr ? dt : 0.0;
         wave_sync();
         double cn = 0.0;
+        if (wave_all(cp == 1.0)) {  // (the last pass's cost scaling was 1, as after most passes: x 1 is exact)
 #pragma unroll
-        for (int j = 0; j < NC; j += 2) {
-            const double2 d2 = *(const double2 *)(S.tmp + j);
-            pr[j] = (dt * (pr[j] * cp)) * d2.x;
-            pr[j + 1] = (dt * (pr[j + 1] * cp)) * d2.y;
-            cn = hwmax(cn, hwmax_abs2(pr[j], pr[j + 1]));
+            for (int j = 0; j < NC; j += 2) {
+                const double2 d2 = *(const double2 *)(S.tmp + j);
+                pr[j] = (dt * pr[j]) * d2.x;
+                pr[j + 1] = (dt * pr[j + 1]) * d2.y;
+                cn = hwmax(cn, hwmax_abs2(pr[j], pr[j + 1]));
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < NC; j += 2) {
+                const double2 d2 = *(const double2 *)(S.tmp + j);
+                pr[j] = (dt * (pr[j] * cp)) * d2.x;
+                pr[j + 1] = (dt * (pr[j + 1] * cp)) * d2.y;
+                cn = hwmax(cn, hwmax_abs2(pr[j], pr[j + 1]));
+            }
         }
         wave_sync();
         if (lr) { Dr *= dt; Er *= et; }
@@ -571,6 +593,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
             if (j >= r) S.Ph()[PL::pk(r, j)] = pr[j];  // the upper triangle, row r by lane r (zero rows beyond N)
         S.Dv()[r] = Dr;
         S.Ev()[r] = Er;
+        S.Ei()[r] = 1.0 / (lr ? Er : 1.0);
+        S.Di()[r] = 1.0 / (lr ? Dr : 1.0);
     }
     {
         const double se = l_ssum<LAY>(Er * Er, lane);  // sum_{i >= r} E_i^2: A^'A^ = 2 K0^2 D_r D_k SE[max(r, k)]
@@ -599,7 +623,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     {
         // |q^| in both scalings: q does not change during the solve, so every check reads these (the check's
         // own arithmetic: DiD = 1 / D_r, the max over the plant's steps)
-        const double qd = (double)qh, DiD = 1.0 / (lr ? Dr : 1.0);
+        const double qd = (double)qh, DiD = 1.0 / (lr ? Dr : 1.0);  // (== S.Di()[r])
         const double qn_r = hwmax(l_max<LAY>(lr ? fabs(qd) : 0.0, lane), 0.0);  // (0 and NaN: as pmax below)
         const double qn_s = hwmax(l_max<LAY>(lr ? fabs(DiD * qd) : 0.0, lane), 0.0);
         if (r == 0) {
@@ -817,29 +841,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         const TD costl = C.sh[0], cinvl = C.sh[1], K0l = C.sh[3];
         const TD xd = (TD)xs, ztd = (TD)zt, zbd = (TD)zb, ytd = (TD)yt, ybd = (TD)yb, dxd = (TD)dx;
         const TD EKd = lr ? Erl * K0l : 0.0, DKd = Ddl * K0l, Ed = lr ? Erl : 0.0;
-        const TD EiD = 1.0 / Erl, DiD = 1.0 / Drl;
+        const TD EiD = lr ? C.Ei()[rc] : 1.0, DiD = lr ? C.Di()[rc] : 1.0;  // (1 / E, 1 / D from the setup)
         const TD utd = lr ? utl * Erl : 0.0, ubd = lr ? ubl * Erl : 0.0;  // (== (T) bounds for fp64)
         const TD ax = EKd * l_psum<LAY>(Ddl * xd, lane);
         const TD aty = DKd * l_ssum<LAY>(Ed * (ytd - ybd), lane);
         const TD px = p_times(xs);
-        TD ax_z = 0, ax_zs = 0, zn_s = 0, zn_r = 0, axn_s = 0, axn_r = 0;
-        TD dr_r = 0, dr_s = 0, atyn_r = 0, atyn_s = 0, pxn_r = 0, pxn_s = 0;
+        // OSQP's tests read ||z|| and ||A x|| only as max(||z||, ||A x||), and ||A' y||, ||P x|| only as
+        // max(||q||, ||A' y||, ||P x||): each pair is one reduction of the lanes' pair maxima (max is exact in
+        // any order), four per norm set instead of six
+        TD ax_z = 0, ax_zs = 0, zax_r = 0, zax_s = 0, dr_r = 0, dr_s = 0, atpx_r = 0, atpx_s = 0;
         const TD qn_r = C.sh[4], qn_s = C.sh[5];
         if (lr) {
             const TD r1 = ax - ztd, r2 = -ax - zbd;
             ax_z = hwmax_abs2(r1, r2);
             ax_zs = hwmax_abs2(EiD * r1, EiD * r2);
-            zn_r = hwmax_abs2(ztd, zbd);
-            zn_s = hwmax_abs2(EiD * ztd, EiD * zbd);
-            axn_r = fabs(ax);
-            axn_s = fabs(EiD * ax);
+            zax_r = hwmax_abs(hwmax_abs2(ztd, zbd), ax);
+            zax_s = hwmax_abs(hwmax_abs2(EiD * ztd, EiD * zbd), EiD * ax);
             const TD rd = (qsl + px) + aty;
             dr_r = fabs(rd);
             dr_s = fabs(DiD * rd);
-            atyn_r = fabs(aty);
-            atyn_s = fabs(DiD * aty);
-            pxn_r = fabs(px);
-            pxn_s = fabs(DiD * px);
+            atpx_r = hwmax_abs2(aty, px);
+            atpx_s = hwmax_abs2(DiD * aty, DiD * px);
         }
         // (OSQP's vec_norm_inf starts from 0 and skips NaN: v_max with 0 returns the non-NaN operand, so a
         // plant whose lanes are all NaN reads 0 in either layout, as OSQP does; the identity on finite norms)
@@ -848,25 +870,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         // else the unscaled ones), and the scaled ones adapt_rho reads: only the sets this iteration uses
         // (wave-uniform; with the default intervals three checks in four test termination only)
         if (scaled_term || at_adapt) {
-            ax_z = pmax(ax_z); zn_r = pmax(zn_r); axn_r = pmax(axn_r);
-            dr_r = pmax(dr_r); atyn_r = pmax(atyn_r); pxn_r = pmax(pxn_r);
+            ax_z = pmax(ax_z); zax_r = pmax(zax_r); dr_r = pmax(dr_r); atpx_r = pmax(atpx_r);
         }
         if (!scaled_term && (at_check || last)) {
-            ax_zs = pmax(ax_zs); zn_s = pmax(zn_s); axn_s = pmax(axn_s);
-            dr_s = pmax(dr_s); atyn_s = pmax(atyn_s); pxn_s = pmax(pxn_s);
+            ax_zs = pmax(ax_zs); zax_s = pmax(zax_s); dr_s = pmax(dr_s); atpx_s = pmax(atpx_s);
         }
         const TD pri_res = scaled_term ? ax_z : ax_zs;
         const TD dua_res = scaled_term ? dr_r : cinvl * dr_s;
 
         // OSQP is_primal_infeasible on delta_y (l = -inf: d = max(dy, 0) on every row); the A^'d product
         // only when some half is a candidate
-        auto primal_infeasible = [&](TD eps) -> bool {
+        // (need: this plant runs and its residual test failed, where OSQP evaluates the certificate; a wave with
+        // no such plant skips it — uniform)
+        auto primal_infeasible = [&](TD eps, bool need) -> bool {
+            if (!wave_any(need)) return false;
             const TD d1 = fmax((TD)dyt, 0.0), d2 = fmax((TD)dyb, 0.0);
             TD ndy = lr ? fmax(fabs(scaled_term ? d1 : Erl * d1), fabs(scaled_term ? d2 : Erl * d2)) : 0.0;
             TD lhs = lr ? utd * d1 + ubd * d2 : 0.0;
             ndy = pmax(ndy);
             lhs = l_sum<LAY>(lhs, lane);
-            const bool cand = ndy > kDivisionTol && lhs < eps * ndy;
+            const bool cand = need && ndy > kDivisionTol && lhs < eps * ndy;
             if (!wave_any(cand)) return false;
             const TD atd = DKd * l_ssum<LAY>(Ed * (d1 - d2), lane);
             const TD nat = pmax(lr ? fabs(scaled_term ? atd : DiD * atd) : 0.0);
@@ -874,11 +897,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         };
         // OSQP is_dual_infeasible on delta_x; the P^ dx and A^ dx products only when some half is a
         // candidate
-        auto dual_infeasible = [&](TD eps) -> bool {
+        auto dual_infeasible = [&](TD eps, bool need) -> bool {
+            if (!wave_any(need)) return false;
             const TD qdx = l_sum<LAY>(lr ? qsl * dxd : 0.0, lane);
             const TD ndx = pmax(lr ? fabs(scaled_term ? dxd : Drl * dxd) : 0.0);
             const TD cs = scaled_term ? 1.0 : costl;
-            const bool cand = ndx > kDivisionTol && qdx < -cs * eps * ndx;
+            const bool cand = need && ndx > kDivisionTol && qdx < -cs * eps * ndx;
             if (!wave_any(cand)) return false;
             const TD t2 = p_times(dx);
             const TD t3 = EKd * l_psum<LAY>(Ddl * dxd, lane);
@@ -892,14 +916,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
             if (pri_res > kInfty || dua_res > kInfty) return kNonCvx;
             const TD ea = st.eps_abs * mul, er = st.eps_rel * mul;
             bool prim_ok = false, dual_ok = false, prim_inf = false, dual_inf = false;
-            const TD ep = ea + er * (scaled_term ? fmax(zn_r, axn_r) : fmax(zn_s, axn_s));
+            const TD ep = ea + er * (scaled_term ? zax_r : zax_s);
             if (pri_res < ep) prim_ok = true;
-            const bool pi = primal_infeasible(st.eps_prim_inf * mul);  // (uniform: evaluated for both halves)
+            const bool pi = primal_infeasible(st.eps_prim_inf * mul, !done && !prim_ok);  // (called uniformly)
             if (!prim_ok) prim_inf = pi;
-            const TD ed = ea + er * (scaled_term ? fmax(fmax(qn_r, atyn_r), pxn_r)
-                                                 : cinvl * fmax(fmax(qn_s, atyn_s), pxn_s));
+            const TD ed = ea + er * (scaled_term ? fmax(qn_r, atpx_r) : cinvl * fmax(qn_s, atpx_s));
             if (dua_res < ed) dual_ok = true;
-            const bool di = dual_infeasible(st.eps_dual_inf * mul);
+            const bool di = dual_infeasible(st.eps_dual_inf * mul, !done && !dual_ok);
             if (!dual_ok) dual_inf = di;
             if (prim_ok && dual_ok) return approx ? kSolvedInaccurate : kSolved;
             if (prim_inf) return approx ? kPrimalInfeasibleInaccurate : kPrimalInfeasible;
@@ -914,8 +937,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         }
         if (!term && at_adapt) {
             const TD rhod = (TD)rho;
-            const TD pr_ = ax_z / (fmax(zn_r, axn_r) + kDivisionTol);
-            const TD dn = fmax(fmax(qn_r, atyn_r), pxn_r);
+            const TD pr_ = ax_z / (zax_r + kDivisionTol);
+            const TD dn = fmax(qn_r, atpx_r);
             const TD du = dr_r / (dn + kDivisionTol);
             TD rn = rhod * sqrt(pr_ / (du + kDivisionTol));
             rn = fmin(fmax(rn, kRhoMin), kRhoMax);
