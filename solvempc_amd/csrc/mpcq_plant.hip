@@ -289,16 +289,64 @@ template <int LAY> __device__ __forceinline__ bool l_any(bool p, int lane)  // a
     }
 }
 
+// Batched reductions over a plant's steps through LDS (the checks' norms and sums): every lane of a step r
+// writes its K values to the plant's rows red[j][r]; lane j of the plant's first 16-lane row reduces row j
+// over the NC steps (dead steps hold 0) — a maximum from 0 with v_max (skipping NaN, as OSQP's
+// vec_norm_inf), or, for bit j of SUM set, a sum in four interleaved partials, (s0 + s1) + (s2 + s3) — and
+// writes it back to red[j][0], which every lane then reads.  One LDS round trip and ~20 VALU for up to
+// four reductions, where a DPP / permute reduction costs ~15 VALU and two LDS permutes each.  The same
+// order in both layouts (LAY 2 and 3 give the same bits).  Call with the whole wave active.
+template <int LAY, int NC, int K, unsigned SUM>
+__device__ __forceinline__ void lay_reduce_k(double *red, double (&v)[K], int r, int lane)
+{
+    static_assert(K >= 1 && K <= 4 && NC % 2 == 0, "four work rows of NC steps");
+    if (r < NC) {
+#pragma unroll
+        for (int j = 0; j < K; j++) red[j * NC + r] = v[j];
+    }
+    wave_sync();
+    const int jr = LAY == 3 ? (lane < 48 ? (lane & 15) : 16) : (lane & 31);
+    if (jr < K) {
+        const double *row = red + jr * NC;
+        double a[4] = {0.0, 0.0, 0.0, 0.0};
+        if ((SUM >> jr) & 1u) {
+#pragma unroll
+            for (int k = 0; k < NC; k += 2) {
+                const double2 x = *(const double2 *)(row + k);
+                a[k & 3] += x.x;
+                a[(k + 1) & 3] += x.y;
+            }
+            a[0] = (a[0] + a[1]) + (a[2] + a[3]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < NC; k += 2) {
+                const double2 x = *(const double2 *)(row + k);
+                a[k & 3] = hwmax(a[k & 3], x.x);
+                a[(k + 1) & 3] = hwmax(a[(k + 1) & 3], x.y);
+            }
+            a[0] = hwmax(hwmax(a[0], a[1]), hwmax(a[2], a[3]));
+        }
+        red[jr * NC] = a[0];
+    }
+    wave_sync();
+#pragma unroll
+    for (int j = 0; j < K; j++) v[j] = red[j * NC];
+    wave_sync();
+}
+
 // Per plant in LDS (fp64).  P^ is kept as its packed upper triangle (row i holds columns i .. N-1 at
 // i NC - i (i - 1) / 2): OSQP's own P, one copy of each entry.  Union region u: first the condensing
 // recurrences' histories V, Cr, then the lag table G (packed like P: G(d, T) for d + T < N), then P^ and
-// the vectors Dv .. piv, each written once what it overlaps is dead.
+// the vectors Dv .. Di, each written once what it overlaps is dead.  Work region w (4 NC): CS and tmp while
+// the plant is condensed and scaled, the pivot row of a Gauss-Jordan step, and the batched reductions of
+// the checks (lay_reduce_k) — never live at the same time.
 template <int NC> struct PlantLds {
     static constexpr int NP = NC * (NC + 1) / 2;
-    static constexpr int NU = (NC + 1) * 16 > NP + 9 * NC ? (NC + 1) * 16 : NP + 9 * NC;
-    static_assert(NP % 2 == 0, "16-B aligned vectors");
+    static constexpr int NV = NP + 8 * NC;
+    static constexpr int NU = (NC + 1) * 16 > NV ? (NC + 1) * 16 : NV;
+    static_assert(NP % 2 == 0 && NU % 2 == 0, "16-B aligned vectors");
     double u[NU];
-    double CS[NC], tmp[NC];
+    double w[4 * NC];
     double sh[6];  // cost, 1 / cost, U, K0, max |q^|, max |D^-1 q^| (the checks' constant norms)
     __device__ double *V() { return u; }
     __device__ double *Cr() { return u + (NC + 1) * 8; }
@@ -310,11 +358,14 @@ template <int NC> struct PlantLds {
     __device__ double *qh() { return u + NP + 3 * NC; }
     __device__ double *Ut() { return u + NP + 4 * NC; }
     __device__ double *Ub() { return u + NP + 5 * NC; }
-    __device__ double *piv() { return u + NP + 6 * NC; }
-    __device__ double *Ei() { return u + NP + 7 * NC; }  // 1 / E, 1 / D (OSQP's Einv, Dinv; 1 beyond N)
-    __device__ double *Di() { return u + NP + 8 * NC; }
-    __device__ const double *Ei() const { return u + NP + 7 * NC; }
-    __device__ const double *Di() const { return u + NP + 8 * NC; }
+    __device__ double *Ei() { return u + NP + 6 * NC; }  // 1 / E, 1 / D (OSQP's Einv, Dinv; 1 beyond N)
+    __device__ double *Di() { return u + NP + 7 * NC; }
+    __device__ double *piv() { return w; }
+    __device__ double *red() { return w; }
+    __device__ double *CS() { return w + NC; }
+    __device__ double *tmp() { return w + 2 * NC; }
+    __device__ const double *Ei() const { return u + NP + 6 * NC; }
+    __device__ const double *Di() const { return u + NP + 7 * NC; }
     __device__ const double *Dv() const { return u + NP; }
     __device__ const double *Ev() const { return u + NP + NC; }
     __device__ const double *qh() const { return u + NP + 3 * NC; }
@@ -469,7 +520,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
             for (int s = 0; s < 8; s++) cab += Cd[s < nx ? s : 0] * (s < nx ? V[r * 8 + s] : 0.0);
         }
         const double cs = l_psum<LAY>(cab, lane);  // Su(i, j) = CS[i - j] = sum_{k <= i - j} CAB[k]
-        if (r < NC) S.CS[r] = lr ? cs : 0.0;
+        if (r < NC) S.CS()[r] = lr ? cs : 0.0;
         wave_sync();
         MPCQ_PTIME(13);
     }
@@ -491,7 +542,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
             for (int c = 0; c < 8; c++)
                 if (c < nx) y += Cr[(r + 1) * 8 + c] * Xv[c];
         }
-        if (r < NC) S.tmp[r] = y;
+        if (r < NC) S.tmp()[r] = y;
     }
     wave_sync();
     // P (setH :250-251: H1 = 2 (LL' Rbar LL + RbarD + Su' Qbar Su), symmetric as computed, so
@@ -501,11 +552,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     // (the recurrences' scratch is dead by now).  Row r stays in registers.
     double *G = S.G();  // G(d, T) at pk(d, d + T), d + T < NC
     {
-        const double ct = lr ? S.CS[r] : 0.0;
+        const double ct = lr ? S.CS()[r] : 0.0;
 #pragma unroll
         for (int d = 0; d < NC; d++) {
             const int td = r + d < NC ? r + d : NC - 1;
-            const double prod = (lr && r + d < N) ? ct * S.CS[td] : 0.0;
+            const double prod = (lr && r + d < N) ? ct * S.CS()[td] : 0.0;
             const double g = l_psum<LAY>(prod, lane);
             if (r + d < NC) G[PL::pk(d, d + r)] = g;
         }
@@ -529,7 +580,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         const double xr = a.xref;
 #pragma unroll
         for (int kk = 0; kk < NC; kk++)  // k = r + kk (fixed trip count: the LDS reads issue together)
-            if (r + kk < N) f += S.CS[kk] * (S.tmp[r + kk < NC ? r + kk : NC - 1] - xr);
+            if (r + kk < N) f += S.CS()[kk] * (S.tmp()[r + kk < NC ? r + kk : NC - 1] - xr);
         qk = (2.0 * Q) * f + Fu * Uv;
     }
     double kx = 0.0;  // K X (Sbar rows < s_rows, :185,208)
@@ -556,13 +607,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         const double va = (aK0 * Dr) * emax, ve = (aK0 * Er) * dpre;
         const double dt = 1.0 / sqrt(limit_scaling_p(fmax(cp * vp, va)));
         const double et = 1.0 / sqrt(limit_scaling_p(ve));
-        if (r < NC) S.tmp[r] = lr ? dt : 0.0;
+        if (r < NC) S.tmp()[r] = lr ? dt : 0.0;
         wave_sync();
         double cn = 0.0;
         if (wave_all(cp == 1.0)) {  // (the last pass's cost scaling was 1, as after most passes: x 1 is exact)
 #pragma unroll
             for (int j = 0; j < NC; j += 2) {
-                const double2 d2 = *(const double2 *)(S.tmp + j);
+                const double2 d2 = *(const double2 *)(S.tmp() + j);
                 pr[j] = (dt * pr[j]) * d2.x;
                 pr[j + 1] = (dt * pr[j + 1]) * d2.y;
                 cn = hwmax(cn, hwmax_abs2(pr[j], pr[j + 1]));
@@ -570,7 +621,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         } else {
 #pragma unroll
             for (int j = 0; j < NC; j += 2) {
-                const double2 d2 = *(const double2 *)(S.tmp + j);
+                const double2 d2 = *(const double2 *)(S.tmp() + j);
                 pr[j] = (dt * (pr[j] * cp)) * d2.x;
                 pr[j + 1] = (dt * (pr[j + 1] * cp)) * d2.y;
                 cn = hwmax(cn, hwmax_abs2(pr[j], pr[j + 1]));
@@ -578,7 +629,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         }
         wave_sync();
         if (lr) { Dr *= dt; Er *= et; }
-        const double mean = l_sum<LAY>(lr ? cn : 0.0, lane) / n;
+        double cb[1] = {lr ? cn : 0.0};
+        lay_reduce_k<LAY, NC, 1, 1u>(S.red(), cb, r, lane);
+        const double mean = cb[0] / n;
         cp = 1.0 / limit_scaling_p(fmax(mean, 1.0));
         cost *= cp;
     }
@@ -624,8 +677,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         // |q^| in both scalings: q does not change during the solve, so every check reads these (the check's
         // own arithmetic: DiD = 1 / D_r, the max over the plant's steps)
         const double qd = (double)qh, DiD = 1.0 / (lr ? Dr : 1.0);  // (== S.Di()[r])
-        const double qn_r = hwmax(l_max<LAY>(lr ? fabs(qd) : 0.0, lane), 0.0);  // (0 and NaN: as pmax below)
-        const double qn_s = hwmax(l_max<LAY>(lr ? fabs(DiD * qd) : 0.0, lane), 0.0);
+        double qb[2] = {lr ? fabs(qd) : 0.0, lr ? fabs(DiD * qd) : 0.0};
+        lay_reduce_k<LAY, NC, 2, 0u>(S.red(), qb, r, lane);
+        const double qn_r = qb[0], qn_s = qb[1];
         if (r == 0) {
             S.sh[0] = cost;
             S.sh[1] = cinv;
@@ -835,7 +889,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         // fp64 one does on its own iterate (half-wave reductions)
         using TD = double;
         const int cl = cold_lane(), rc = lay_row<LAY>(cl);
-        const PL &C = lds[lay_plant<LAY>(cl)];
+        PL &C = lds[lay_plant<LAY>(cl)];
         const TD Erl = lr ? C.Ev()[rc] : 1.0, Drl = lr ? C.Dv()[rc] : 1.0, Ddl = lr ? Drl : 0.0, qsl = lr ? C.qh()[rc] : 0.0;
         const TD utl = lr ? C.Ut()[rc] : 0.0, ubl = lr ? C.Ub()[rc] : 0.0;
         const TD costl = C.sh[0], cinvl = C.sh[1], K0l = C.sh[3];
@@ -863,51 +917,73 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
             atpx_r = hwmax_abs2(aty, px);
             atpx_s = hwmax_abs2(DiD * aty, DiD * px);
         }
-        // (OSQP's vec_norm_inf starts from 0 and skips NaN: v_max with 0 returns the non-NaN operand, so a
-        // plant whose lanes are all NaN reads 0 in either layout, as OSQP does; the identity on finite norms)
-        auto pmax = [&](TD v) { return hwmax(l_max<LAY>(v, lane), 0.0); };
         // the norms in the scaling the termination test reads (scaled_termination: OSQP's scaled residuals,
         // else the unscaled ones), and the scaled ones adapt_rho reads: only the sets this iteration uses
-        // (wave-uniform; with the default intervals three checks in four test termination only)
+        // (wave-uniform; with the default intervals three checks in four test termination only), four maxima
+        // per batch (lay_reduce_k: from 0, skipping NaN, as OSQP's vec_norm_inf)
+        double *red = C.red();
         if (scaled_term || at_adapt) {
-            ax_z = pmax(ax_z); zax_r = pmax(zax_r); dr_r = pmax(dr_r); atpx_r = pmax(atpx_r);
+            double b[4] = {ax_z, zax_r, dr_r, atpx_r};
+            lay_reduce_k<LAY, NC, 4, 0u>(red, b, rc, lane);
+            ax_z = b[0]; zax_r = b[1]; dr_r = b[2]; atpx_r = b[3];
         }
         if (!scaled_term && (at_check || last)) {
-            ax_zs = pmax(ax_zs); zax_s = pmax(zax_s); dr_s = pmax(dr_s); atpx_s = pmax(atpx_s);
+            double b[4] = {ax_zs, zax_s, dr_s, atpx_s};
+            lay_reduce_k<LAY, NC, 4, 0u>(red, b, rc, lane);
+            ax_zs = b[0]; zax_s = b[1]; dr_s = b[2]; atpx_s = b[3];
         }
         const TD pri_res = scaled_term ? ax_z : ax_zs;
         const TD dua_res = scaled_term ? dr_r : cinvl * dr_s;
 
-        // OSQP is_primal_infeasible on delta_y (l = -inf: d = max(dy, 0) on every row); the A^'d product
-        // only when some half is a candidate
-        // (need: this plant runs and its residual test failed, where OSQP evaluates the certificate; a wave with
-        // no such plant skips it — uniform)
+        // OSQP's certificates (is_primal_infeasible on delta_y: l = -inf, so d = max(dy, 0) on every row;
+        // is_dual_infeasible on delta_x), evaluated only where a running plant's residual test failed (need),
+        // as OSQP does.  Their norms and sums do not depend on eps: one batch (||dy||, ||dx||, u'd, q'dx) and,
+        // for candidates, one more (||A' d||, ||P dx||), shared by every check_termination call of the iteration.
+        const TD d1 = fmax((TD)dyt, 0.0), d2 = fmax((TD)dyb, 0.0);
+        TD ndy = 0, ndx = 0, lhs = 0, qdx = 0, nat = 0, npdx = 0, sv = 0;
+        bool have1 = false, have_p = false, have_d = false;
+        auto cert1 = [&]() {
+            if (have1) return;
+            have1 = true;
+            double b[4] = {lr ? fmax(fabs(scaled_term ? d1 : Erl * d1), fabs(scaled_term ? d2 : Erl * d2)) : 0.0,
+                           lr ? fabs(scaled_term ? dxd : Drl * dxd) : 0.0, lr ? utd * d1 + ubd * d2 : 0.0,
+                           lr ? qsl * dxd : 0.0};
+            lay_reduce_k<LAY, NC, 4, 0xCu>(red, b, rc, lane);
+            ndy = b[0]; ndx = b[1]; lhs = b[2]; qdx = b[3];
+        };
+        auto cert2 = [&](bool want_p, bool want_d) {  // (uniform flags)
+            double b[2] = {0.0, 0.0};
+            if (want_p && !have_p) {
+                const TD atd = DKd * l_ssum<LAY>(Ed * (d1 - d2), lane);
+                b[0] = lr ? fabs(scaled_term ? atd : DiD * atd) : 0.0;
+            }
+            if (want_d && !have_d) {
+                const TD t2 = p_times(dx);
+                const TD t3 = EKd * l_psum<LAY>(Ddl * dxd, lane);
+                b[1] = lr ? fabs(scaled_term ? t2 : DiD * t2) : 0.0;
+                sv = scaled_term ? t3 : EiD * t3;
+            }
+            lay_reduce_k<LAY, NC, 2, 0u>(red, b, rc, lane);
+            if (want_p && !have_p) nat = b[0];
+            if (want_d && !have_d) npdx = b[1];
+            have_p = have_p || want_p;
+            have_d = have_d || want_d;
+        };
         auto primal_infeasible = [&](TD eps, bool need) -> bool {
             if (!wave_any(need)) return false;
-            const TD d1 = fmax((TD)dyt, 0.0), d2 = fmax((TD)dyb, 0.0);
-            TD ndy = lr ? fmax(fabs(scaled_term ? d1 : Erl * d1), fabs(scaled_term ? d2 : Erl * d2)) : 0.0;
-            TD lhs = lr ? utd * d1 + ubd * d2 : 0.0;
-            ndy = pmax(ndy);
-            lhs = l_sum<LAY>(lhs, lane);
+            cert1();
             const bool cand = need && ndy > kDivisionTol && lhs < eps * ndy;
             if (!wave_any(cand)) return false;
-            const TD atd = DKd * l_ssum<LAY>(Ed * (d1 - d2), lane);
-            const TD nat = pmax(lr ? fabs(scaled_term ? atd : DiD * atd) : 0.0);
+            if (!have_p) cert2(true, false);
             return cand && nat < eps * ndy;
         };
-        // OSQP is_dual_infeasible on delta_x; the P^ dx and A^ dx products only when some half is a
-        // candidate
         auto dual_infeasible = [&](TD eps, bool need) -> bool {
             if (!wave_any(need)) return false;
-            const TD qdx = l_sum<LAY>(lr ? qsl * dxd : 0.0, lane);
-            const TD ndx = pmax(lr ? fabs(scaled_term ? dxd : Drl * dxd) : 0.0);
+            cert1();
             const TD cs = scaled_term ? 1.0 : costl;
             const bool cand = need && ndx > kDivisionTol && qdx < -cs * eps * ndx;
             if (!wave_any(cand)) return false;
-            const TD t2 = p_times(dx);
-            const TD t3 = EKd * l_psum<LAY>(Ddl * dxd, lane);
-            const TD npdx = pmax(lr ? fabs(scaled_term ? t2 : DiD * t2) : 0.0);
-            const TD sv = scaled_term ? t3 : EiD * t3;
+            if (!have_d) cert2(false, true);
             const bool viol = l_any<LAY>(lr && (sv > eps * ndx || -sv > eps * ndx), lane);  // rows r (u finite), N + r (-A x)
             return cand && npdx < cs * eps * ndx && !viol;
         };
