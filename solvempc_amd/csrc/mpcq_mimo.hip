@@ -853,18 +853,22 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
             const double x = vx, zt = vzt, zb = vzb, yt = vyt, yb = vyb;
             const double D = vD, E = vE;
             const double xv = has_sol ? x * D : __builtin_nan("");
-            if (a.x) a.x[(size_t)b * n + e] = xv;
+            // (the element index laundered here: hoisted out of the solve loop, the eight store addresses
+            // were held across it and spilled to scratch, ~40 KB of writes per QP)
+            const int eo = opaque(e);
+            const size_t on = (size_t)b * n + eo, om = (size_t)b * m + eo;
+            if (a.x) a.x[on] = xv;
             if (a.y) {
                 const double cinv = cfg(7);
-                a.y[(size_t)b * m + e] = has_sol ? (yt * E) * cinv : __builtin_nan("");
-                a.y[(size_t)b * m + n + e] = has_sol ? (yb * E) * cinv : __builtin_nan("");
+                a.y[om] = has_sol ? (yt * E) * cinv : __builtin_nan("");
+                a.y[om + n] = has_sol ? (yb * E) * cinv : __builtin_nan("");
             }
             if (k == 0 && status == kSolved) a.U[(size_t)b * NU + c] = a.U[(size_t)b * NU + c] + xv;
-            a.xs[(size_t)b * n + e] = keep ? x : 0.0;
-            a.zs[(size_t)b * m + e] = keep ? zt : 0.0;
-            a.zs[(size_t)b * m + n + e] = keep ? zb : 0.0;
-            a.ys[(size_t)b * m + e] = keep ? yt : 0.0;
-            a.ys[(size_t)b * m + n + e] = keep ? yb : 0.0;
+            a.xs[on] = keep ? x : 0.0;
+            a.zs[om] = keep ? zt : 0.0;
+            a.zs[om + n] = keep ? zb : 0.0;
+            a.ys[om] = keep ? yt : 0.0;
+            a.ys[om + n] = keep ? yb : 0.0;
         }
         if (t == 0) {
             a.rhos[b] = rho;
@@ -1189,38 +1193,34 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
         int ctl = 0;  // 0 continue, 1 refactor, 2 done
         if (info) {
             // ---- update_info: residuals (scaled norms _r, unscaled _s as OSQP reports them)
-            double v[14];
+            // OSQP's tests read ||z||, ||A x|| only as max(||z||, ||A x||) and ||q||, ||A' y||, ||P x|| only as
+            // their maximum: one reduction of the lanes' maxima each (max is exact in any order), eight
+            // values per check instead of fourteen
+            double v[8];
             {
                 const double ax = A_of(valid ? vx : 0.0);
                 const double zt = vzt, zb = vzb, ei = 1.0 / vE;
                 const double rt = ax - zt, rbm = -ax - zb;
-                v[0] = fmax(fabs(rt), fabs(rbm));                 // ax_z
-                v[1] = fmax(fabs(ei * rt), fabs(ei * rbm));       // ax_zs
-                v[2] = fmax(fabs(zt), fabs(zb));                  // zn_r
-                v[3] = fmax(fabs(ei * zt), fabs(ei * zb));        // zn_s
-                v[4] = fabs(ax);                                  // axn_r
-                v[5] = fabs(ei * ax);                             // axn_s
+                v[0] = fmax(fabs(rt), fabs(rbm));                                  // ax_z
+                v[1] = fmax(fabs(ei * rt), fabs(ei * rbm));                        // ax_zs
+                v[2] = fmax(fmax(fabs(zt), fabs(zb)), fabs(ax));                   // max(zn_r, axn_r)
+                v[3] = fmax(fmax(fabs(ei * zt), fabs(ei * zb)), fabs(ei * ax));    // max(zn_s, axn_s)
             }
             {
                 const double aty = At_of(valid ? vyt - vyb : 0.0);
                 const double qh = vqh, px = vpx, di = 1.0 / vD;
                 const double r = (qh + px) + aty;
-                v[6] = fabs(r);         // dr_r
-                v[7] = fabs(di * r);    // dr_s
-                v[8] = fabs(qh);        // qn_r
-                v[9] = fabs(di * qh);   // qn_s
-                v[10] = fabs(aty);      // atyn_r
-                v[11] = fabs(di * aty); // atyn_s
-                v[12] = fabs(px);       // pxn_r
-                v[13] = fabs(di * px);  // pxn_s
+                v[4] = fabs(r);                                                    // dr_r
+                v[5] = fabs(di * r);                                               // dr_s
+                v[6] = fmax(fmax(fabs(qh), fabs(aty)), fabs(px));                  // max(qn_r, atyn_r, pxn_r)
+                v[7] = fmax(fmax(fabs(di * qh), fabs(di * aty)), fabs(di * px));   // max(qn_s, atyn_s, pxn_s)
             }
             if (!valid)
 #pragma unroll
-                for (int i = 0; i < 14; i++) v[i] = 0.0;
+                for (int i = 0; i < 8; i++) v[i] = 0.0;
             block_reduce(v, 0u);
-            const double ax_z = v[0], ax_zs = v[1], zn_r = v[2], zn_s = v[3], axn_r = v[4], axn_s = v[5];
-            const double dr_r = v[6], dr_s = v[7], qn_r = v[8], qn_s = v[9], atyn_r = v[10], atyn_s = v[11];
-            const double pxn_r = v[12], pxn_s = v[13];
+            const double ax_z = v[0], ax_zs = v[1], zax_r = v[2], zax_s = v[3];
+            const double dr_r = v[4], dr_s = v[5], qap_r = v[6], qap_s = v[7];
             const double cinv = cfg(7);
             const bool scaled_term = cfg(5) != 0.0;
             const double pri_res = scaled_term ? ax_z : ax_zs;
@@ -1267,9 +1267,8 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
                 const double mul = approx ? 10.0 : 1.0;
                 const double ea = cfg(0) * mul, er = cfg(1) * mul;
                 if (pri_res > kInfty || dua_res > kInfty) return kNonCvx;
-                const double ep = ea + er * (scaled_term ? fmax(zn_r, axn_r) : fmax(zn_s, axn_s));
-                const double ed = ea + er * (scaled_term ? fmax(fmax(qn_r, atyn_r), pxn_r)
-                                                         : cinv * fmax(fmax(qn_s, atyn_s), pxn_s));
+                const double ep = ea + er * (scaled_term ? zax_r : zax_s);
+                const double ed = ea + er * (scaled_term ? qap_r : cinv * qap_s);
                 const bool pok = pri_res < ep, dok = dua_res < ed;
                 if (pok && dok) return approx ? kSolvedInaccurate : kSolved;
                 if (!pok && primal_inf(cfg(2) * mul))
@@ -1285,8 +1284,8 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
                 if (pass == 0) {
                     if (at_check || last) status = check(false);
                     if (status == kUnsolved && at_adapt && !last) {  // adapt_rho (scaled norms)
-                        const double pr = ax_z / (fmax(zn_r, axn_r) + kDivisionTol);
-                        const double dn = fmax(fmax(qn_r, atyn_r), pxn_r);
+                        const double pr = ax_z / (zax_r + kDivisionTol);
+                        const double dn = qap_r;
                         const double du = dr_r / (dn + kDivisionTol);
                         double rn = rho * sqrt(pr / (du + kDivisionTol));
                         rn = fmin(fmax(rn, kRhoMin), kRhoMax);
