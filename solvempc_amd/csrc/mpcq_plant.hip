@@ -440,9 +440,10 @@ __device__ __forceinline__ bool gj_rows(double (&row)[NC], double *piv, int n, i
 
 // WPE: waves per SIMD the register allocation is held to (2, or 3 for A/B: MPCQ_PLANT_WPE); LAY: plants per
 // wave (2: one per 32-lane half; 3: N <= 20, rows plus interleaved tails, see lay3_*)
-template <typename T, int NC, int WPE, int LAY>
+template <typename T, int NC, int WPE, int LAY, int NXC>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? WPE : 2, NC <= 20 ? 8 : 4))) void plant_step_kernel(PlantStepArgs a)
 {
+    static_assert(NXC == 4 || NXC == 8, "states: nx <= 4 (the cart-pole of the reference) or <= 8");
     static_assert(NC % 4 == 0, "broadcast rows are read 16 B at a time");
     static_assert(LAY == 2 || (LAY == 3 && NC <= 20), "three plants per wave: N <= 20");
     using PL = PlantLds<NC>;
@@ -483,9 +484,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     double *V = S.V(), *Cr = S.Cr();  // V[k][8], Cr[k][8] for k <= N (the union region)
     {
         const double *Ad = a.Ad + (size_t)p * nx * nx, *Bd = a.Bd + (size_t)p * nx, *Cd = a.Cd + (size_t)p * nx;
-        double adr[8], adc[8];  // row t and column t of Ad
+        double adr[NXC], adc[NXC];  // row t and column t of Ad
 #pragma unroll
-        for (int s = 0; s < 8; s++) {
+        for (int s = 0; s < NXC; s++) {
             adr[s] = (r < nx && s < nx) ? Ad[r * nx + s] : 0.0;
             adc[s] = (r < nx && s < nx) ? Ad[s * nx + r] : 0.0;
         }
@@ -499,7 +500,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
             // (two FMA chains per product: the step's latency is the LDS round trip plus four FMAs)
             double v0 = 0.0, v1 = 0.0, c0 = 0.0, c1 = 0.0;
 #pragma unroll
-            for (int s = 0; s < 8; s += 2) {
+            for (int s = 0; s < NXC; s += 2) {
                 v0 = fma(adr[s], V[k * 8 + s], v0);
                 v1 = fma(adr[s + 1], V[k * 8 + s + 1], v1);
                 c0 = fma(Cr[k * 8 + s], adc[s], c0);
@@ -517,7 +518,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         double cab = 0.0;  // Cd Ad^r Bd
         if (lr) {
 #pragma unroll
-            for (int s = 0; s < 8; s++) cab += Cd[s < nx ? s : 0] * (s < nx ? V[r * 8 + s] : 0.0);
+            for (int s = 0; s < NXC; s++) cab += Cd[s < nx ? s : 0] * (s < nx ? V[r * 8 + s] : 0.0);
         }
         const double cs = l_psum<LAY>(cab, lane);  // Su(i, j) = CS[i - j] = sum_{k <= i - j} CAB[k]
         if (r < NC) S.CS()[r] = lr ? cs : 0.0;
@@ -528,10 +529,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     const double *K = a.K + (size_t)p * nx;
     const double K0 = K[0];
     // this step's inputs (controllerStep: X, U)
-    double Xv[8];
+    double Xv[NXC];
     const double *Xp = a.X + (size_t)p * nx;
 #pragma unroll
-    for (int c = 0; c < 8; c++) Xv[c] = c < nx ? Xp[c] : 0.0;
+    for (int c = 0; c < NXC; c++) Xv[c] = c < nx ? Xp[c] : 0.0;
     const double Uv = a.U[p];
     // the free response (Sx X)_k = Cd Ad^(k+1) X, lane k: with it q = Fx X + Fu U + Fr 1 xref (setF,
     // :374; Fx = 2 Su' Qbar Sx, :307) is 2 Q sum_{k >= r} CS[k - r] ((Sx X)_k - xref) + Fu U
@@ -539,43 +540,43 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         double y = 0.0;
         if (lr) {
 #pragma unroll
-            for (int c = 0; c < 8; c++)
+            for (int c = 0; c < NXC; c++)
                 if (c < nx) y += Cr[(r + 1) * 8 + c] * Xv[c];
         }
         if (r < NC) S.tmp()[r] = y;
     }
     wave_sync();
     // P (setH :250-251: H1 = 2 (LL' Rbar LL + RbarD + Su' Qbar Su), symmetric as computed, so
-    // (H1 + H1') / 2 = H1): (Su'Su)(r, j) = sum_{k >= max(r,j)} CS[k - r] CS[k - j] = G(|r - j|, N - 1 -
-    // max(r, j)) with G(d, T) = sum_{t <= T} CS[t] CS[t + d]: lane t forms CS[t] CS[t + d] for every lag
-    // d, one prefix scan per lag gives G(d, .) across the lanes, and lane r gathers its row from LDS
-    // (the recurrences' scratch is dead by now).  Row r stays in registers.
-    double *G = S.G();  // G(d, T) at pk(d, d + T), d + T < NC
+    // (H1 + H1') / 2 = H1): H = Su'Su, H(r, j) = sum_{k >= max(r,j)} CS[k - r] CS[k - j], by the diagonal
+    // recurrence H(r, j) = H(r + 1, j + 1) + CS[N-1-r] CS[N-1-j] (the k = N - 1 term; H(N, .) = 0): one row
+    // per step from r = N - 1 up, lane j >= r forming H(r, j) from the row below (one LDS read, one FMA and
+    // one write per lane and step), the upper triangle packed in G (the recurrences' scratch is dead by
+    // now); lane r then gathers its row from LDS.  Row r stays in registers.
+    double *H = S.G();
     {
-        const double ct = lr ? S.CS()[r] : 0.0;
-#pragma unroll
-        for (int d = 0; d < NC; d++) {
-            const int td = r + d < NC ? r + d : NC - 1;
-            const double prod = (lr && r + d < N) ? ct * S.CS()[td] : 0.0;
-            const double g = l_psum<LAY>(prod, lane);
-            if (r + d < NC) G[PL::pk(d, d + r)] = g;
+        const double cj = lr ? S.CS()[N - 1 - r] : 0.0;  // CS[N-1-j], j = this lane's step
+        for (int rr = N - 1; rr >= 0; rr--) {
+            const double crr = S.CS()[N - 1 - rr];
+            const bool on = lr && r >= rr;
+            const double below = (on && r + 1 < N) ? H[PL::pk(rr + 1, r + 1)] : 0.0;
+            if (on) H[PL::pk(rr, r)] = fma(crr, cj, below);
+            wave_sync();
         }
     }
-    wave_sync();
     MPCQ_PTIME(14);
     double pr[NC];
 #pragma unroll
     for (int j = 0; j < NC; j++) {
         double v = 0.0;
         if (lr && j < N) {
-            const int mx = r > j ? r : j, d = r > j ? r - j : j - r;
-            v = 2.0 * ((R * (double)(N - mx) + (r == j ? RD : 0.0)) + Q * G[PL::pk(d, d + N - 1 - mx)]);
+            const int mx = r > j ? r : j;
+            v = 2.0 * ((R * (double)(N - mx) + (r == j ? RD : 0.0)) + Q * H[PL::pk(r, j)]);
         }
         pr[j] = v;
     }
     double qk = 0.0;
     if (lr) {
-        const double Fu = 2.0 * (R + Q * G[PL::pk(r, N - 1)]);  // Fu[r] (:305, incl. the diagonal() quirk: R 1)
+        const double Fu = 2.0 * (R + Q * H[PL::pk(0, r)]);  // Fu[r] (:305, incl. the diagonal() quirk: R 1)
         double f = 0.0;
         const double xr = a.xref;
 #pragma unroll
@@ -585,7 +586,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     }
     double kx = 0.0;  // K X (Sbar rows < s_rows, :185,208)
 #pragma unroll
-    for (int c = 0; c < 8; c++)
+    for (int c = 0; c < NXC; c++)
         if (c < nx) kx += K[c] * Xv[c];
 
     MPCQ_PTIME(2);
@@ -1047,14 +1048,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
 #undef MPCQ_PTIME
 #undef MPCQ_PSTAMP
 
+template <typename T, int NC, int LAY, int NXC>
+int plant_step_launch_x(const PlantStepArgs &a, hipStream_t s)
+{
+    const dim3 grid((a.n_plants + LAY - 1) / LAY), block(64);
+    if (NC <= 20 && a.wpe == 3) hipLaunchKernelGGL((plant_step_kernel<T, NC, 3, LAY, NXC>), grid, block, 0, s, a);
+    else if (NC <= 20 && a.wpe == 4) hipLaunchKernelGGL((plant_step_kernel<T, NC, 4, LAY, NXC>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((plant_step_kernel<T, NC, 2, LAY, NXC>), grid, block, 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+// nx <= 4 (the reference's cart-pole): the state loops at four components; else eight
 template <typename T, int NC, int LAY>
 int plant_step_launch_l(const PlantStepArgs &a, hipStream_t s)
 {
-    const dim3 grid((a.n_plants + LAY - 1) / LAY), block(64);
-    if (NC <= 20 && a.wpe == 3) hipLaunchKernelGGL((plant_step_kernel<T, NC, 3, LAY>), grid, block, 0, s, a);
-    else if (NC <= 20 && a.wpe == 4) hipLaunchKernelGGL((plant_step_kernel<T, NC, 4, LAY>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((plant_step_kernel<T, NC, 2, LAY>), grid, block, 0, s, a);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
+    return a.nx <= 4 ? plant_step_launch_x<T, NC, LAY, 4>(a, s) : plant_step_launch_x<T, NC, LAY, 8>(a, s);
 }
 // N in 17 .. 20: three plants per wave unless PlantStepArgs::layout asks for two (test hook)
 template <typename T, int NC>
