@@ -383,41 +383,69 @@ template <int NC> struct PlantLds {
     __device__ static int pk_row(int r, int i, int q) { return i < r ? i * NC - (i * (i - 1)) / 2 - i + r : q + i; }
 };
 
-// Gauss-Jordan inverse of this half's SPD matrix (n x n; SPD: no pivoting), lane r holding row r in
-// registers.  Per pivot the owner publishes its row p through LDS (one wave: the DS queue keeps the
-// order, wave_sync only pins the compiler's); then every lane updates its row in place without a branch:
-// row <- fma(-g, p, s row) with (s, g) = (1, row[k] / p[k]) on the other rows and (1 / p[k], 0) on the
-// pivot row (a multiply by 1 and an fma with 0 are exact), and element k <- -g, or 1 / p[k] on the pivot
-// row.  Two VALU per element per pivot.
+// Gauss-Jordan inverse of this plant's SPD matrix (n x n; SPD: no pivoting) on pivot pairs K = {k, k + 1},
+// lane r holding row r in registers.  The two owners publish rows p0 = row k, p1 = row k + 1 through LDS
+// (one wave: the DS queue keeps the order, wave_sync only pins the compiler's); every lane forms
+// A_KK^-1 = [d, -b; -b, a] / (a d - b^2) from them and updates its row without a branch:
+//     row <- fma(-g0, p0, fma(-g1, p1, s row)),   row[k], row[k + 1] <- -g0, -g1,
+// with s = 1, [g0 g1] = [row[k] row[k + 1]] A_KK^-1 on the other rows (A - A(:,K) A_KK^-1 A(K,:), columns K
+// -A(:,K) A_KK^-1) and s = 0, [g0 g1] = -(row k or k + 1 of A_KK^-1) on the pivot rows (rows K <- A_KK^-1
+// A(K,:), whose columns K are then A_KK^-1).  Half the serial LDS round trips of one pivot per step and
+// three VALU per element per pair where single pivots take four.  An odd n ends on a single pivot.
 template <int NC>
 __device__ __forceinline__ bool gj_rows(double (&row)[NC], double *piv, int n, int r)
 {
     bool ok = true;
 #pragma unroll
-    for (int k = 0; k < NC; k++) {
+    for (int k = 0; k < NC; k += 2) {
         if (k >= n) continue;  // (uniform; continue keeps the loop fully unrollable)
-        if (r == k) {
+        const bool pair = k + 1 < n;
+        if (r == k || (pair && r == k + 1)) {
+            double *dst = piv + (r - k) * NC;
 #pragma unroll
-            for (int j = 0; j < NC; j += 2) *(double2 *)(piv + j) = make_double2(row[j], row[j + 1]);
+            for (int j = 0; j < NC; j += 2) *(double2 *)(dst + j) = make_double2(row[j], row[j + 1]);
         }
         wave_sync();
-        const double pk = piv[k];
-        // 1 / pk by v_rcp_f64 and two Newton steps (within an ulp; the inverse is compared with the oracle's
-        // LDL solve at tolerance, not bitwise): five VALU where the IEEE division takes ten
-        double ip = __builtin_amdgcn_rcp(pk);
-        ip = fma(ip, fma(-pk, ip, 1.0), ip);
-        ip = fma(ip, fma(-pk, ip, 1.0), ip);
-        if (!(pk > 0.0)) ok = false;
-        const bool pr = r == k;
-        const double sc = pr ? ip : 1.0, g = pr ? 0.0 : row[k] * ip;
+        const double *p0 = piv, *p1 = piv + NC;
+        const double a = p0[k];
+        double g0, g1, sc;
+        if (pair) {
+            const double b = p0[k + 1], d = p1[k + 1];
+            const double det = fma(a, d, -(b * b));
+            if (!(a > 0.0) || !(det > 0.0)) ok = false;
+            // 1 / det by v_rcp_f64 and two Newton steps (within an ulp; the inverse is compared with the oracle's
+            // LDL solve at tolerance, not bitwise)
+            double id = __builtin_amdgcn_rcp(det);
+            id = fma(id, fma(-det, id, 1.0), id);
+            id = fma(id, fma(-det, id, 1.0), id);
+            const double ikk = d * id, ikl = -b * id, ill = a * id;
+            const double f0 = row[k], f1 = row[k + 1];
+            const bool pk0 = r == k, pk1 = r == k + 1;
+            sc = (pk0 || pk1) ? 0.0 : 1.0;
+            g0 = pk0 ? -ikk : pk1 ? -ikl : fma(f0, ikk, f1 * ikl);
+            g1 = pk0 ? -ikl : pk1 ? -ill : fma(f0, ikl, f1 * ill);
+        } else {  // the last pivot of an odd n
+            if (!(a > 0.0)) ok = false;
+            double ip = __builtin_amdgcn_rcp(a);
+            ip = fma(ip, fma(-a, ip, 1.0), ip);
+            ip = fma(ip, fma(-a, ip, 1.0), ip);
+            const bool pk0 = r == k;
+            sc = pk0 ? 0.0 : 1.0;
+            g0 = pk0 ? -ip : row[k] * ip;
+            g1 = 0.0;
+        }
 #pragma unroll
         for (int j = 0; j < NC; j += 2) {
-            const double2 m2 = *(const double2 *)(piv + j);
-            const double mk[2] = {m2.x, m2.y};
+            const double2 m0 = *(const double2 *)(p0 + j);
+            const double2 m1 = *(const double2 *)(p1 + j);
+            const double q0[2] = {m0.x, m0.y}, q1[2] = {m1.x, m1.y};
 #pragma unroll
             for (int e = 0; e < 2; e++) {
                 const int jj = j + e;
-                row[jj] = (jj == k) ? (pr ? ip : -g) : fma(-g, mk[e], row[jj] * sc);
+                if (jj == k) row[jj] = -g0;
+                else if (jj == k + 1 && pair) row[jj] = -g1;
+                else if (pair) row[jj] = fma(-g0, q0[e], fma(-g1, q1[e], row[jj] * sc));
+                else row[jj] = fma(-g0, q0[e], row[jj] * sc);
             }
         }
         wave_sync();
@@ -482,8 +510,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     // CAB[k] = Cd Ad^k Bd and c_k = Cd Ad^k (Sx row k-1) by the recurrences v_{k+1} = Ad v_k,
     // c_{k+1} = c_k Ad: lane t < nx of the half owns component t (scratch in the P^ slot).
     double *V = S.V(), *Cr = S.Cr();  // V[k][8], Cr[k][8] for k <= N (the union region)
+    // every global read of the plant's data and inputs issued here, together (each phase reading its own
+    // at its point of use waited a full memory latency, four times per wave)
+    const double *Cd = a.Cd + (size_t)p * nx;
+    double cdv[NXC], Kv[NXC], Xv[NXC];
+    const double *K = a.K + (size_t)p * nx, *Xp = a.X + (size_t)p * nx;
+#pragma unroll
+    for (int c = 0; c < NXC; c++) {
+        cdv[c] = c < nx ? Cd[c] : 0.0;
+        Kv[c] = c < nx ? K[c] : 0.0;
+        Xv[c] = c < nx ? Xp[c] : 0.0;
+    }
+    const double Q = a.Q[p], R = a.R[p], RD = a.RD[p], Uv = a.U[p];
+    const double K0 = Kv[0];
     {
-        const double *Ad = a.Ad + (size_t)p * nx * nx, *Bd = a.Bd + (size_t)p * nx, *Cd = a.Cd + (size_t)p * nx;
+        const double *Ad = a.Ad + (size_t)p * nx * nx, *Bd = a.Bd + (size_t)p * nx;
         double adr[NXC], adc[NXC];  // row t and column t of Ad
 #pragma unroll
         for (int s = 0; s < NXC; s++) {
@@ -518,22 +559,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         double cab = 0.0;  // Cd Ad^r Bd
         if (lr) {
 #pragma unroll
-            for (int s = 0; s < NXC; s++) cab += Cd[s < nx ? s : 0] * (s < nx ? V[r * 8 + s] : 0.0);
+            for (int s = 0; s < NXC; s++) cab += cdv[s] * (s < nx ? V[r * 8 + s] : 0.0);
         }
         const double cs = l_psum<LAY>(cab, lane);  // Su(i, j) = CS[i - j] = sum_{k <= i - j} CAB[k]
         if (r < NC) S.CS()[r] = lr ? cs : 0.0;
         wave_sync();
         MPCQ_PTIME(13);
     }
-    const double Q = a.Q[p], R = a.R[p], RD = a.RD[p];
-    const double *K = a.K + (size_t)p * nx;
-    const double K0 = K[0];
-    // this step's inputs (controllerStep: X, U)
-    double Xv[NXC];
-    const double *Xp = a.X + (size_t)p * nx;
-#pragma unroll
-    for (int c = 0; c < NXC; c++) Xv[c] = c < nx ? Xp[c] : 0.0;
-    const double Uv = a.U[p];
+    // (this step's inputs, controllerStep's X and U, are Xv and Uv above)
     // the free response (Sx X)_k = Cd Ad^(k+1) X, lane k: with it q = Fx X + Fu U + Fr 1 xref (setF,
     // :374; Fx = 2 Su' Qbar Sx, :307) is 2 Q sum_{k >= r} CS[k - r] ((Sx X)_k - xref) + Fu U
     {
@@ -587,7 +620,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     double kx = 0.0;  // K X (Sbar rows < s_rows, :185,208)
 #pragma unroll
     for (int c = 0; c < NXC; c++)
-        if (c < nx) kx += K[c] * Xv[c];
+        if (c < nx) kx += Kv[c] * Xv[c];
 
     MPCQ_PTIME(2);
     // ---------------------------------------------------------------- 2. scale_data (Ruiz)
