@@ -195,26 +195,45 @@ __device__ __forceinline__ double lane_fetch(double v, int src4)
     const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute(src4, (int)(unsigned)(u >> 32));
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
-// LAY 3 inclusive prefix / suffix over a plant's steps (op with identity 0, as half_prefix / half_suffix)
-template <typename T, typename F> __device__ __forceinline__ T lay3_prefix(T v, F op, int lane)
+// LAY 3 inclusive prefix / suffix over a plant's steps (op with identity 0, as half_prefix / half_suffix).
+// The one- and two-step shifts run on rows 0 .. 2 only, and a disabled row keeps the DPP destination's old
+// value, which must be 0 there: `z` is a register whose row-3 lanes hold 0 and stay 0 (every write to it is
+// one of these row-masked moves), so the moves take it as their old operand in place instead of a freshly
+// zeroed copy (two v_mov per step and half of a 64-bit value).  Callers in the solve loop keep one z across
+// iterations.
+template <typename T, typename F> __device__ __forceinline__ T lay3_prefix(T v, F op, int lane, T &z)
 {
-    v = op(v, dppm<0x111, 0x7, 0xF>(T(0), v));  // row_shr 1, 2: rows 0 .. 2 only
-    v = op(v, dppm<0x112, 0x7, 0xF>(T(0), v));
+    z = dppm<0x111, 0x7, 0xF>(z, v);  // row_shr 1, 2: rows 0 .. 2 only (row 3 reads z's 0)
+    v = op(v, z);
+    z = dppm<0x112, 0x7, 0xF>(z, v);
+    v = op(v, z);
     v = op(v, dppm<0x114, 0xF, 0xF>(T(0), v));  // row_shr 4, 8: rows 0 .. 2, and row 3's steps 16 + k - 1, - 2
     v = op(v, dppm<0x118, 0xF, 0xF>(T(0), v));
     // a tail lane adds its plant's row total (lane 16 h + 15); row lanes read lane 63's zero
     const int src = lane >= 48 ? 16 * (lane & 3) + 15 : 63;
     return op(v, lane_fetch(v, 4 * src));
 }
-template <typename T, typename F> __device__ __forceinline__ T lay3_suffix(T v, F op, int lane)
+template <typename T, typename F> __device__ __forceinline__ T lay3_suffix(T v, F op, int lane, T &z)
 {
-    v = op(v, dppm<0x101, 0x7, 0xF>(T(0), v));  // row_shl 1, 2: rows 0 .. 2 only
-    v = op(v, dppm<0x102, 0x7, 0xF>(T(0), v));
+    z = dppm<0x101, 0x7, 0xF>(z, v);  // row_shl 1, 2: rows 0 .. 2 only
+    v = op(v, z);
+    z = dppm<0x102, 0x7, 0xF>(z, v);
+    v = op(v, z);
     v = op(v, dppm<0x104, 0xF, 0xF>(T(0), v));  // row_shl 4, 8: and row 3's steps 16 + k + 1, + 2
     v = op(v, dppm<0x108, 0xF, 0xF>(T(0), v));
     // a row lane adds its plant's tail suffix (step 16: lane 48 + h); tail lanes read lane 63's zero
     const int src = lane < 48 ? 48 + (lane >> 4) : 63;
     return op(v, lane_fetch(v, 4 * src));
+}
+template <typename T, typename F> __device__ __forceinline__ T lay3_prefix(T v, F op, int lane)
+{
+    T z = T(0);
+    return lay3_prefix(v, op, lane, z);
+}
+template <typename T, typename F> __device__ __forceinline__ T lay3_suffix(T v, F op, int lane)
+{
+    T z = T(0);
+    return lay3_suffix(v, op, lane, z);
 }
 // LAY 3 reduction over a plant's steps, every lane of the plant ending on the same bits (as half_reduce:
 // the row butterfly, the tail's pairs (16, 17), (18, 19) then their sum, then row total op tail total)
@@ -242,6 +261,17 @@ template <int LAY, typename T> __device__ __forceinline__ T l_psum(T v, int lane
 template <int LAY, typename T> __device__ __forceinline__ T l_ssum(T v, int lane)
 {
     if constexpr (LAY == 3) return lay3_suffix(v, [](T a, T b) { return a + b; }, lane);
+    else return ssum(v, lane);
+}
+// (the solve loop's forms: z as in lay3_prefix, unused by the two-plant layout)
+template <int LAY, typename T> __device__ __forceinline__ T l_psum(T v, int lane, T &z)
+{
+    if constexpr (LAY == 3) return lay3_prefix(v, [](T a, T b) { return a + b; }, lane, z);
+    else return psum(v);
+}
+template <int LAY, typename T> __device__ __forceinline__ T l_ssum(T v, int lane, T &z)
+{
+    if constexpr (LAY == 3) return lay3_suffix(v, [](T a, T b) { return a + b; }, lane, z);
     else return ssum(v, lane);
 }
 template <int LAY, typename T> __device__ __forceinline__ T l_prefix_max(T v, int lane)
@@ -810,6 +840,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     int next_check = ct ? ct : -1, next_adapt = ai ? ai : -1;
     int it = 0;
     bool done = false, setup_ok = true, first = true, refactor = true;
+    T z3 = T(0);  // the loop's scans' DPP destination, 0 on row 3 (lay3_prefix)
+    // the loop's broadcast rows, addressed from a lane index laundered here: a fresh live range after the
+    // setup's register peak (formed at entry and held across the setup, the address was spilled and
+    // reloaded from scratch every iteration)
+    T *bxl, *bwl;
+    {
+        const int ln = opaque(lane);
+        const int hl = (LAY == 3 && lay3_noplant(ln)) ? NB - 1 : lay_plant<LAY>(ln);
+        bxl = bx[hl];
+        bwl = bw[hl];
+    }
 
     auto finalize = [&]() {
         const int cl = cold_lane(), r = lay_row<LAY>(cl);
@@ -877,18 +918,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         const T wt = tt_fma(rho, zt, -yt) - tt_fma(rho, zb, -yb);
         T xi;
         if constexpr (MERGED) {
-            const T atw = (DT * K0T) * l_ssum<LAY>(ET * wt, lane);  // A^'(w_top - w_bot)
-            if (r < NC) bxh[r] = tt_fma(sigT, xs, atw);  // (0 on a row beyond N: x = 0, D = 0)
+            const T atw = (DT * K0T) * l_ssum<LAY>(ET * wt, lane, z3);  // A^'(w_top - w_bot)
+            if (r < NC) bxl[r] = tt_fma(sigT, xs, atw);  // (0 on a row beyond N: x = 0, D = 0)
             wave_sync();
-            xi = row_dot(Srow, bxh, gk);
+            xi = row_dot(Srow, bxl, gk);
             wave_sync();
         } else {
             if (r < NC) {
-                bxh[r] = lr ? xs : T(0);
-                bwh[r] = lr ? wt : T(0);
+                bxl[r] = lr ? xs : T(0);
+                bwl[r] = lr ? wt : T(0);
             }
             wave_sync();
-            xi = row_dot(Srow, bxh, gk) + row_dot(Btc, bwh, T(0));
+            xi = row_dot(Srow, bxl, gk) + row_dot(Btc, bwl, T(0));
             wave_sync();
         }
         const T xn = tt_fma(alpha, xi, oma * xs);  // (0 on a row beyond N: zero M^-1 row, g = 0)
@@ -900,7 +941,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         // z~ = A^ x~ (top rows; bottom = -top), relaxation, projection onto [l, u], dual update
         T ETl = ET;
         asm volatile("" : "+v"(ETl));
-        const T zz = (ETl * K0T) * l_psum<LAY>(DT * xi, lane);
+        const T zz = (ETl * K0T) * l_psum<LAY>(DT * xi, lane, z3);
         T dyt, dyb;
         {
             T v = tt_fma(alpha, zz, oma * zt);
