@@ -674,22 +674,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         if (r < NC) S.tmp()[r] = lr ? dt : 0.0;
         wave_sync();
         double cn = 0.0;
-        if (wave_all(cp == 1.0)) {  // (the last pass's cost scaling was 1, as after most passes: x 1 is exact)
+        // (a uniform branch on cp == 1 saved the 20 cost multiplies but its two paths' row registers met in
+        // 20 moves: measured no gain, one path kept)
 #pragma unroll
-            for (int j = 0; j < NC; j += 2) {
-                const double2 d2 = *(const double2 *)(S.tmp() + j);
-                pr[j] = (dt * pr[j]) * d2.x;
-                pr[j + 1] = (dt * pr[j + 1]) * d2.y;
-                cn = hwmax(cn, hwmax_abs2(pr[j], pr[j + 1]));
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < NC; j += 2) {
-                const double2 d2 = *(const double2 *)(S.tmp() + j);
-                pr[j] = (dt * (pr[j] * cp)) * d2.x;
-                pr[j + 1] = (dt * (pr[j + 1] * cp)) * d2.y;
-                cn = hwmax(cn, hwmax_abs2(pr[j], pr[j + 1]));
-            }
+        for (int j = 0; j < NC; j += 2) {
+            const double2 d2 = *(const double2 *)(S.tmp() + j);
+            pr[j] = (dt * (pr[j] * cp)) * d2.x;
+            pr[j + 1] = (dt * (pr[j + 1] * cp)) * d2.y;
+            cn = hwmax(cn, hwmax_abs2(pr[j], pr[j + 1]));
         }
         wave_sync();
         if (lr) { Dr *= dt; Er *= et; }
