@@ -20,6 +20,7 @@ for wl in cfg2 perplant quadrotor stream; do
   (cd "$out" && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d prof_$wl -o run -- python3 "$root/bench.py" \
       --workload $wl --steps $steps --warmup 1 --variants 0 --cpu-seconds 0 --cfg3-strong 0 > prof_$wl.log 2>&1) \
     || { echo "prof $wl failed"; tail -20 "$out/prof_$wl.log"; exit 1; }
+  python3 tools/rocpd_export.py "$out/prof_$wl/run_results.db" "$out/${tag}_$wl" > /dev/null || exit 1
   echo "prof $wl ok"
 done
 exit 0
