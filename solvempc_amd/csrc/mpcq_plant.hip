@@ -662,11 +662,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     const double aK0 = fabs(K0);
     double Dr = lr ? 1.0 : 0.0, Er = lr ? 1.0 : 0.0;  // (0 on dead lanes: neutral in every scan)
     double cost = 1.0, cp = 1.0;
-    for (int it = 0; it < st.scaling; it++) {
-        double vq[4] = {0.0, 0.0, 0.0, 0.0};  // (max is exact in any order: four short chains)
+    // the row maximum max_j |P_rj| of the current (cost-unscaled) rows: the first pass forms it, every later
+    // pass takes the previous pass's cn, the maximum of the same values (max is exact in any order)
+    double vp;
+    {
+        double vq[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int j = 0; j < NC; j++) vq[j & 3] = hwmax_abs(vq[j & 3], pr[j]);
-        const double vp = hwmax(hwmax(vq[0], vq[1]), hwmax(vq[2], vq[3]));
+        vp = hwmax(hwmax(vq[0], vq[1]), hwmax(vq[2], vq[3]));
+    }
+    for (int it = 0; it < st.scaling; it++) {
         const double emax = l_suffix_max<LAY>(Er, lane), dpre = l_prefix_max<LAY>(Dr, lane);
         const double va = (aK0 * Dr) * emax, ve = (aK0 * Er) * dpre;
         const double dt = 1.0 / sqrt(limit_scaling_p(fmax(cp * vp, va)));
@@ -684,6 +689,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
             cn = hwmax(cn, hwmax_abs2(pr[j], pr[j + 1]));
         }
         wave_sync();
+        vp = cn;
         if (lr) { Dr *= dt; Er *= et; }
         double cb[1] = {lr ? cn : 0.0};
         lay_reduce_k<LAY, NC, 1, 1u>(S.red(), cb, r, lane);
