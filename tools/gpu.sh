@@ -31,13 +31,13 @@ for step in "$@"; do
       timeout -k 10 600 python -u tools/order_probe.py $arg > "$out/probe_$arg.log" 2>&1 \
         || { echo "probe failed"; tail -20 "$out/probe_$arg.log"; exit 1; } ;;
     prof)
-      (cd "$out" && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d prof -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 3 --variants 0 --cpu-seconds 0 $arg \
+      (cd "$out" && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d prof -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 3 --variants 0 --cpu-seconds 0 --cfg3-strong 0 $arg \
         > prof.log 2>&1) || { echo "prof failed"; tail -20 "$out/prof.log"; exit 1; } ;;
     pmc)  # pmc:<workload>,<dtype>[,<extra PMC set>] -> $out/pmc_<workload>_<dtype>/ (FETCH, WRITE, MFMA/VALU passes)
       IFS=, read -r wl dt extra <<< "$arg"
       sets=$'FETCH_SIZE\nWRITE_SIZE\nSQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE'
       [ -n "$extra" ] && sets="$sets"$'\n'"${extra//+/ }"
-      CMD="python bench.py --workload $wl --dtype $dt --steps 3 --warmup 1 --cpu-seconds 0 --variants 0" \
+      CMD="python bench.py --workload $wl --dtype $dt --steps 3 --warmup 1 --cpu-seconds 0 --variants 0 --cfg3-strong 0" \
         PMC_SETS="$sets" timeout -k 10 600 bash tools/pmc.sh "$dt" "$out/pmc_${wl}_$dt" > "$out/pmc_${wl}_$dt.log" 2>&1 \
         || { echo "pmc failed"; cat "$out/pmc_${wl}_$dt/passes.txt"; exit 1; } ;;
     stamps)  # stamps:mimo_setup -> per-stage cycles of mimo_setup_kernel on the debug library built here
@@ -61,7 +61,7 @@ for step in "$@"; do
       done ;;
     pmcw)  # pmcw:VAR=val,<dtype> -> one WRITE_SIZE pass of the cfg2 bench with the test hook set
       IFS=, read -r ev dt <<< "$arg"
-      env "$ev" CMD="python bench.py --dtype $dt --steps 3 --warmup 1 --cpu-seconds 0 --variants 0" PMC_SETS=WRITE_SIZE \
+      env "$ev" CMD="python bench.py --dtype $dt --steps 3 --warmup 1 --cpu-seconds 0 --variants 0 --cfg3-strong 0" PMC_SETS=WRITE_SIZE \
         timeout -k 10 300 bash tools/pmc.sh "$dt" "$out/pmcw_${ev}_$dt" > "$out/pmcw_${ev}_$dt.log" 2>&1 \
         || { echo "pmcw failed"; cat "$out/pmcw_${ev}_$dt/passes.txt"; exit 1; } ;;
     *) echo "unknown step $step"; exit 2 ;;

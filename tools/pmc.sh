@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT" || exit 2
 export TMPDIR=/tmp
 dt=${1:-f32}; out=${2:-gpurun_out/pmc_$dt}
 mkdir -p "$out"
-CMD=${CMD:-"python bench.py --steps 3 --warmup 1 --dtype $dt --cpu-seconds 0"}
+CMD=${CMD:-"python bench.py --steps 3 --warmup 1 --dtype $dt --cpu-seconds 0 --cfg3-strong 0"}
 i=0
 while read -r set; do
   [ -z "$set" ] && continue
