@@ -944,8 +944,7 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
         double s0[4], s1[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) s0[i] = s1[i] = 0.0;
-        const double2 *v2 = (const double2 *)(in + kSegLd * (opaque(t) & 7));  // (column group re-derived here:
-                                                                             // held across the solve it was spilled)
+        const double2 *v2 = (const double2 *)(in + kSegLd * cg);
         double2 q0 = v2[0], q1 = v2[1];
 #pragma unroll
         for (int h = 0; h < 4; h++) {  // 4-column chunks (register budget), the next one in flight
