@@ -615,14 +615,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     // per step from r = N - 1 up, lane j >= r forming H(r, j) from the row below (one LDS read, one FMA and
     // one write per lane and step), the upper triangle packed in G (the recurrences' scratch is dead by
     // now); lane r then gathers its row from LDS.  Row r stays in registers.
+    // Two rows per step: row rr - 1 by the same recurrence from H(rr, j + 1), which the lane forms itself from
+    // row rr + 1 with the operands lane j + 1 uses for it (the same bits as one row per step), so ten LDS round
+    // trips instead of twenty.
     double *H = S.G();
     {
-        const double cj = lr ? S.CS()[N - 1 - r] : 0.0;  // CS[N-1-j], j = this lane's step
-        for (int rr = N - 1; rr >= 0; rr--) {
-            const double crr = S.CS()[N - 1 - rr];
-            const bool on = lr && r >= rr;
-            const double below = (on && r + 1 < N) ? H[PL::pk(rr + 1, r + 1)] : 0.0;
-            if (on) H[PL::pk(rr, r)] = fma(crr, cj, below);
+        const double cj = lr ? S.CS()[N - 1 - r] : 0.0;                      // CS[N-1-j], j = this lane's step
+        const double cj1 = (lr && r + 1 < N) ? S.CS()[N - 2 - r] : 0.0;       // CS[N-1-(j+1)]
+        for (int rr = N - 1; rr >= 0; rr -= 2) {
+            const double crr = S.CS()[N - 1 - rr], crm = rr >= 1 ? S.CS()[N - rr] : 0.0;  // rows rr, rr - 1
+            const bool on = lr && r >= rr, on1 = lr && rr >= 1 && r >= rr - 1;
+            const double b1 = (on1 && r + 1 < N && rr + 1 < N) ? H[PL::pk(rr + 1, r + 1)] : 0.0;  // H(rr+1, j+1)
+            const double b2 = (on1 && r + 2 < N && rr + 1 < N) ? H[PL::pk(rr + 1, r + 2)] : 0.0;  // H(rr+1, j+2)
+            if (on) H[PL::pk(rr, r)] = fma(crr, cj, b1);                  // H(rr, j)
+            if (on1) {
+                const double hr1 = r + 1 < N ? fma(crr, cj1, b2) : 0.0;    // H(rr, j+1), as lane j + 1 forms it
+                H[PL::pk(rr - 1, r)] = fma(crm, cj, hr1);                  // H(rr-1, j)
+            }
             wave_sync();
         }
     }
