@@ -625,7 +625,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
         for (int rr = N - 1; rr >= 0; rr -= 2) {
             const double crr = S.CS()[N - 1 - rr], crm = rr >= 1 ? S.CS()[N - rr] : 0.0;  // rows rr, rr - 1
             const bool on = lr && r >= rr, on1 = lr && rr >= 1 && r >= rr - 1;
-            const double b1 = (on1 && r + 1 < N && rr + 1 < N) ? H[PL::pk(rr + 1, r + 1)] : 0.0;  // H(rr+1, j+1)
+            const double b1 = ((on || on1) && r + 1 < N && rr + 1 < N) ? H[PL::pk(rr + 1, r + 1)] : 0.0;  // H(rr+1, j+1)
             const double b2 = (on1 && r + 2 < N && rr + 1 < N) ? H[PL::pk(rr + 1, r + 2)] : 0.0;  // H(rr+1, j+2)
             if (on) H[PL::pk(rr, r)] = fma(crr, cj, b1);                  // H(rr, j)
             if (on1) {
