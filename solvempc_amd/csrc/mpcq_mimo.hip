@@ -851,8 +851,7 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
         const bool keep = has_sol || status == kInvalidBounds || status == kTypeChanged;
         if (valid) {
             const double x = vx, zt = vzt, zb = vzb, yt = vyt, yb = vyb;
-            const int vio = opaque(vi);  // (this lane's D, E from LDS: their registers were spilled for the finalize)
-            const double D = s_D[vio], E = s_E[vio];
+            const double D = vD, E = vE;
             const double xv = has_sol ? x * D : __builtin_nan("");
             // (the element index laundered here: hoisted out of the solve loop, the eight store addresses
             // were held across it and spilled to scratch, ~40 KB of writes per QP)
@@ -890,8 +889,7 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
     // rows row_nat(i), columns 16 cg + j (P^ rows are padded to L.ldp: aligned, in-bounds loads);
     // the padding beyond n is the identity
     auto load_P = [&]() {
-        const int cgl = opaque(t) & 7;  // (re-derived: see gemv_rows)
-        const int seg = 16 * cgl < L.ldp - 16 ? 16 * cgl : L.ldp - 16;
+        const int seg = 16 * cg < L.ldp - 16 ? 16 * cg : L.ldp - 16;
         const int r = rg_here();
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -900,7 +898,7 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
 #pragma unroll
             for (int j = 0; j < 8; j++) {
                 const double2 v = row[j];
-                const int gj = 16 * cgl + 2 * j;
+                const int gj = 16 * cg + 2 * j;
                 Mb[i][2 * j] = (gi < n && gj < n) ? v.x : (gi == gj ? 1.0 : 0.0);
                 Mb[i][2 * j + 1] = (gi < n && gj + 1 < n) ? v.y : (gi == gj + 1 ? 1.0 : 0.0);
             }
@@ -975,11 +973,10 @@ __global__ __launch_bounds__(kMimoThreads, MPCQ_MIMO_WAVES_PER_EU) void mimo_sol
     auto gemv = [&](const double *in, double *outv) {
         double part[4];
         gemv_rows(in, part);
-        const int tl = opaque(t), rgl = tl >> 3;  // (re-derived, as in gemv_rows)
-        if ((tl & 7) == 0)
+        if (cg == 0)
 #pragma unroll
             for (int i = 0; i < 4; i++)
-                if (row_nat(rgl, i) < n) outv[row_cmp(rgl, i) * 32 + row_blk(rgl, i)] = part[i];
+                if (row_nat(rg, i) < n) outv[row_cmp(rg, i) * 32 + row_blk(rg, i)] = part[i];
     };
     // ONE: this lane's element (block k, component c) of M . in, from lane 8 (k >> 2) + (k & 3) of the
     // same wave, whose register row (its cg & 3) is block k
