@@ -1260,11 +1260,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 // fp32 stretch: iterations it + 1 .. nxt - mix_r on fp32 copies of the state (yt = y / rho),
                 // the operators rounded from the fp64 images; then the last mix_r - 1 plain iterations and
                 // the info iteration in fp64 (below)
-                const int n32 = nxt - a.mix_r;
+                const int n32 = mix64 ? it : nxt - a.mix_r;  // (mix64: no fp32 stretch)
 #ifdef MPCQ_MIX_STAMPS  // debug build: cycles in the fp32 stretches -> phase stamp 5
                 const long long t_mix = a.stamps ? (long long)__builtin_amdgcn_s_memtime() : 0;
 #endif
-                if (it < n32 && !mix64) {
+                if (it < n32) {
                     float xs32[G][NS], z32[G][MS], y32[G][MS], uh32[G][MS], gv32[G][NS], rho32[G], adk32[G][KNR];
 #pragma unroll
                     for (int gi = 0; gi < G; gi++) {
@@ -1593,7 +1593,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
         MPCQ_INFO_MARK(2);
 
         // OSQP is_primal_infeasible on delta_y = dy (this iteration's dual step), per group.
-        auto primal_infeasible = [&](T eps, const bool (&need)[G], bool (&res)[G]) {
+        auto primal_infeasible = [&](T eps, const bool (&need)[G], bool (&res)[G], bool track) {
             {  // no column of the wave asks (every live one primal-feasible): nothing to screen
                 bool anyn = false;
 #pragma unroll
@@ -1653,7 +1653,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 if constexpr (MIX) near = near || (cand[gi] && !res[gi] && nat < T(1e4) * eps * ndy[gi]);
             }
             if constexpr (MIX) {
-                if (wave_any(near)) mix64 = true;
+                if (track && wave_any(near)) mix64 = true;
             }
         };
         // OSQP is_dual_infeasible on delta_x^ = W dx, per group.
@@ -1754,7 +1754,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC, O
                 dual_ok[gi] = dua_res[gi] < ed;
                 need_d[gi] = need && !dual_ok[gi];
             }
-            primal_infeasible(approx ? a.eps10[2] : (T)st.eps_prim_inf, need_p, prim_inf);
+            primal_infeasible(approx ? a.eps10[2] : (T)st.eps_prim_inf, need_p, prim_inf, !approx);
             dual_infeasible(approx ? a.eps10[3] : (T)st.eps_dual_inf, need_d, dual_inf);
 #pragma unroll
             for (int gi = 0; gi < G; gi++) {
