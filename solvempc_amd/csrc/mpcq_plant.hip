@@ -779,18 +779,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 20 ? W
     constexpr bool MERGED = std::is_same<T, double>::value;
     T Srow[NC], Btc[MERGED ? 1 : NC];
     T gk = T(0);
-    const double Dd = lr ? Dr : 0.0, A2 = 2.0 * K0 * K0;
+    const double Dd = lr ? Dr : 0.0;
     auto factor = [&](double rho) -> bool {
         const int cl = cold_lane(), r = lay_row<LAY>(cl);
         PL &S = lds[lay_plant<LAY>(cl)];
         double row[NC];
         const int q = PL::row_q(r);
+        // (D_r, K0 read back from LDS here: the loop's registers for them were spilled for this cold path)
+        const double K0c = S.sh[3], A2c = 2.0 * K0c * K0c, Ddc = lr ? S.Dv()[r] : 0.0;
 #pragma unroll
         for (int j = 0; j < NC; j++) {
             double v = 0.0;
             if (lr && j < n) {
                 const int mx = r > j ? r : j;
-                v = S.Ph()[PL::pk_row(r, j, q)] + (r == j ? st.sigma : 0.0) + rho * (((A2 * Dd) * S.Dv()[j]) * S.SE()[mx]);
+                v = S.Ph()[PL::pk_row(r, j, q)] + (r == j ? st.sigma : 0.0) + rho * (((A2c * Ddc) * S.Dv()[j]) * S.SE()[mx]);
             }
             row[j] = v;
         }
