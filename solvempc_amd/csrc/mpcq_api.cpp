@@ -1578,9 +1578,35 @@ static int launch_tile_stream(mpcq_ctx *c, hipStream_t s, double *X, double *U, 
     a.img = (const T *)c->d_img;
     a.stop_iter = INT_MAX;
     a.sim = sa;
+    // debug build: per-wave stage stamps of the launch (tools/stamps.py format, one phase), written to
+    // $MPCQ_TILE_STAMPS after it
+    const char *stp = debug_hook("MPCQ_TILE_STAMPS");
+    const size_t swaves = (size_t)waves + 8;  // (+ a workgroup's idle waves)
+    if (stp && *stp) {
+        if (c->d_stamps) (void)hipFree(c->d_stamps);
+        c->d_stamps = nullptr;
+        if (hipMalloc((void **)&c->d_stamps, 8 * 8 * swaves) != hipSuccess ||
+            hipMemsetAsync(c->d_stamps, 0, 8 * 8 * swaves, s) != hipSuccess)
+            return -2;
+        a.stamps = c->d_stamps;
+    }
     const int rc = std::is_same<T, float>::value
                        ? mpcq_internal_tile_stream_launch_f32((const mpcq::AdmmArgs<float> *)&a, c->KN, c->KM, s)
                        : mpcq_internal_tile_stream_launch_f64((const mpcq::AdmmArgs<double> *)&a, c->KN, c->KM, s);
+    if (rc == 0 && stp && *stp) {
+        std::vector<long long> h(8 * swaves);
+        if (hipMemcpyAsync(h.data(), c->d_stamps, 8 * h.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -2;
+        if (FILE *f = std::fopen(stp, "wb")) {
+            const long long hdr[2] = {1, (long long)swaves};
+            std::fwrite(hdr, 8, 2, f);
+            std::fwrite(h.data(), 8, h.size(), f);
+            std::fclose(f);
+        }
+        (void)hipFree(c->d_stamps);
+        c->d_stamps = nullptr;
+    }
     if (rc == 0) {
         c->qu_lazy = true;
         c->lazy_xref = xref;

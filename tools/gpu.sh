@@ -50,6 +50,12 @@ for step in "$@"; do
         python bench.py --dtype $arg --steps 1 --warmup 1 --cpu-seconds 0 --variants 0 > "$out/tstamps_bench_$arg.json" 2>&1 \
         && python tools/stamps.py "$out/tstamps_$arg.bin" > "$out/tstamps_$arg.txt" 2>&1 \
         || { echo "tstamps failed"; tail "$out/tstamps_bench_$arg.json"; exit 1; } ;;
+    sstamps)  # sstamps:<dtype> -> per-wave stamps of the one-launch stream (config 5; debug library tools/dbg_r06s,
+              # built here: SRC=mpcq_tile_f64.hip DBGDIR=tools/dbg_r06s bash tools/build_dbg.sh MPCQ_INFO_STAMPS)
+      MPCQ_LIBRARY=tools/dbg_r06s/libmpcq.so MPCQ_TILE_STAMPS="$out/sstamps_$arg.bin" timeout -k 10 300 \
+        python bench.py --workload stream --dtype $arg --steps 1 --warmup 1 --cpu-seconds 0 --variants 0 > "$out/sstamps_bench_$arg.json" 2>&1 \
+        && python tools/stamps.py "$out/sstamps_$arg.bin" > "$out/sstamps_$arg.txt" 2>&1 \
+        || { echo "sstamps failed"; tail "$out/sstamps_bench_$arg.json"; exit 1; } ;;
     calib)  # WRITE_SIZE calibration of the finalize's store patterns (tools/calib/write_calib.hip, built here)
       (cd "$out" && timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d calib -o run -- "$GRAFT_REPO_ROOT/tools/calib/write_calib" \
         > calib.log 2>&1) || { echo "calib failed"; tail "$out/calib.log"; exit 1; } ;;
